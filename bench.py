@@ -1,0 +1,193 @@
+"""Headline benchmark: MCDO gated-attention MIL inference on MI355X.
+
+Metric (BASELINE.json): bags/sec x MCDO-samples (T=100) at N=2048, d=512 -- BASELINE config 3
+(N=2048 instances/bag, L=d=512, D=128, C=2 heads, separate attention as config.yml:8, T=100,
+bf16 operands, fp32 accumulate / softmax / outputs). A step = one pass of the hot path over one
+batch of --bags synthetic bags per GPU already resident in HBM: gate-score kernel (all T
+samples, Philox masks in-register) + softmax/pooling + per-bag attention mean/var, and for
+N > 1 GPUs the gather of the per-bag predictions Y[T, C] to every rank (weak scaling: every
+rank owns --bags bags).
+
+Prints ONE JSON line (rank 0). `roofline` prices the dominant kernel (gate_scores) with the
+ALGORITHMIC FLOPs of the literal reference computation against the bf16 dense
+MFMA peak; its time comes from HIP events around that kernel on the launch stream.
+`cpu_baseline` times the reference op sequence (oracle/mcdo_ref.py, torch CPU, with its own
+dropout RNG) on a bounded sample of the same workload on this host.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "montecarlo-gated-mil_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "bags/sec × MCDO-samples (T=100) at N=2048,d=512; 1/2/4/8-GPU + %HBM roofline"
+PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}   # MI355X dense MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def flops_per_bag(N, T, L, D, C, G):
+    # T * [2*N*L*D*2G + 2*N*D*C + 2*N*L*C + 2*L*C]
+    return T * (2 * N * L * D * 2 * G + 2 * N * D * C + 2 * N * L * C + 2 * L * C)
+
+
+def bytes_per_bag(N, T, L, C, esize):
+    # features read once + A[T,C,N] written + Y[T,C] written (weights once per launch, added below)
+    return N * L * esize + 4 * T * C * N + 4 * T * C
+
+
+def cpu_baseline(N, T, L, D, C, shared, budget_s):
+    """The reference CPU path (torch op sequence incl. dropout RNG), bounded sample."""
+    from oracle import mcdo_ref, synthetic
+    arrays = synthetic.head_arrays(synthetic.head_state_dict(0, L=L, D=D, C=C, shared=shared), C, shared)
+    prm = mcdo_ref.HeadParams(arrays)
+    H = synthetic.bag_features(42, N, L)
+    threads = torch.get_num_threads()
+    with torch.no_grad():
+        mcdo_ref.mc_inference_torch_rng(H, prm, T, 0.1, 0.1)   # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            mcdo_ref.mc_inference_torch_rng(H, prm, T, 0.1, 0.1)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or n >= 50:
+                break
+    return {"value": n * T / el, "unit": "bag-samples/s", "cores": threads, "kind": "port",
+            "sample": f"{n} bags of N={N}, T={T}, fp32, {'shared' if shared else 'separate'} "
+                      f"attention, torch {torch.__version__} CPU, {threads} threads, "
+                      f"{el * 1e3 / n:.1f} ms/bag"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--bags", type=int, default=16, help="bags per GPU per step")
+    ap.add_argument("--n", type=int, default=2048)
+    ap.add_argument("--T", type=int, default=100)
+    ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
+    ap.add_argument("--shared", type=int, default=0)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from mcgmil import _lib, ops
+    from oracle import synthetic  # seeded synthetic parameters only (not a compute path)
+    lib = _lib.load()
+
+    N, T, L, D, C = args.n, args.T, 512, 128, 2
+    G = 1 if args.shared else C
+    B = args.bags
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    esize = 2 if args.dtype == "bf16" else 4
+
+    # synthetic, random-init weights of the reference architecture; features |N(0,1)|
+    sd = synthetic.head_state_dict(0, L=L, D=D, C=C, shared=bool(args.shared))
+    arrays = synthetic.head_arrays(sd, C, bool(args.shared))
+    head = ops.HeadTensors(*[torch.from_numpy(arrays[k]).to(dev) for k in ops.HeadTensors._fields])
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    H = torch.randn(B * N, L, device=dev, generator=g).abs_().to(dt).contiguous()
+    offs = ops.bag_offsets_tensor([N] * B, dev)
+    bag_ids = torch.arange(rank * B, (rank + 1) * B, dtype=torch.int32, device=dev)
+    packed = ops.packed_weights(head, dt)
+
+    a = ops.make_args(H, offs, head, T, C, G, D, 0.1, 0.1, seed=42, bag_ids=bag_ids)
+    a.packed_w = ctypes.c_void_p(packed.data_ptr())
+    Y = torch.empty(B, T, C, device=dev)
+    A = torch.empty(T * C * B * N, device=dev)
+    Am = torch.empty(C * B * N, device=dev)
+    Av = torch.empty(C * B * N, device=dev)
+    a.Y, a.A = ctypes.c_void_p(Y.data_ptr()), ctypes.c_void_p(A.data_ptr())
+    a.A_mean, a.A_var = ctypes.c_void_p(Am.data_ptr()), ctypes.c_void_p(Av.data_ptr())
+    n = ctypes.c_size_t()
+    _lib.check(lib.mcgmil_workspace_size(ctypes.byref(a), ctypes.byref(n)), "workspace_size")
+    ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
+    a.workspace, a.workspace_bytes = ctypes.c_void_p(ws.data_ptr()), n.value
+    pa = ctypes.byref(a)
+    stream = torch.cuda.current_stream(dev)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    gather = [torch.empty_like(Y) for _ in range(world)] if world > 1 else None
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        _lib.check(lib.mcgmil_gate_scores(pa, sh), "gate_scores")
+        if ev is not None:
+            ev[1].record(stream)
+        _lib.check(lib.mcgmil_softmax_pool(pa, sh), "softmax_pool")
+        _lib.check(lib.mcgmil_bag_stats(pa, sh), "bag_stats")
+        if gather is not None:
+            dist.all_gather(gather, Y)
+
+    for _ in range(args.warmup):
+        step()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    gate_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / args.steps
+    if world > 1:
+        t = torch.tensor([el, gate_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, gate_ms = float(t[0]), float(t[1])
+
+    total_bag_samples = world * B * T * args.steps
+    value = total_bag_samples / el
+    F = flops_per_bag(N, T, L, D, C, G) * B
+    achieved = F / (gate_ms * 1e-3) / 1e12
+    hbm_bytes = bytes_per_bag(N, T, L, C, esize) * B + packed.numel()
+    hbm_gbs = hbm_bytes / (gate_ms * 1e-3) / 1e9
+    if rank == 0:
+        cpu = None if args.no_cpu_baseline else cpu_baseline(N, T, L, D, C, bool(args.shared),
+                                                             args.cpu_budget)
+        out = {
+            "metric": METRIC, "value": value, "unit": "bag-samples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.dtype, "data": "synthetic (|N(0,1)| features, random-init head)",
+            "config": {"workload": f"BASELINE config 3: N={N} instances/bag, d={L}, D={D}, C={C}, "
+                                   f"T={T} MCDO samples, {'shared' if args.shared else 'separate'} "
+                                   f"attention, {args.dtype} operands / fp32 accumulate",
+                       "bags_per_gpu_per_step": B, "global_batch_bags": world * B,
+                       "N": N, "L": L, "D": D, "C": C, "T": T, "parallelism": f"bags over {world} GPU(s)"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[args.dtype],
+                         "unit": "TFLOP/s", "frac": achieved / PEAK_TFLOPS[args.dtype],
+                         "traffic": None, "kernel": "gate_scores_kernel",
+                         "kernel_ms": gate_ms, "algorithmic_tflop_per_launch": F / 1e12},
+            "roofline_hbm": {"achieved": hbm_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": hbm_gbs / PEAK_HBM_GBS,
+                             "algorithmic_bytes_per_launch": hbm_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

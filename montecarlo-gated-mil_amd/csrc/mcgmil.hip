@@ -1,0 +1,304 @@
+// C ABI (include/mcgmil.h) over the gfx950 MCDO kernels: validation, workspace layout,
+// kernel selection and stream-ordered launches. No allocation, no host synchronisation.
+#include <math.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+
+#include "../../include/mcgmil.h"
+#include "mcgmil_kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(MCGMIL_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+uint32_t drop_threshold(float p) {
+    // identical to oracle_drop_threshold (oracle/philox_oracle.c), p taken as double
+    const double pd = (double)p;
+    if (!(pd > 0.0)) return 0u;
+    const double x = floor(pd * 65536.0 + 0.5);
+    return x >= 65536.0 ? 65536u : (uint32_t)x;
+}
+
+float dropout_scale(float p) {
+    // torch's nn.Dropout factor: 1.0f / (float)(1 - p) (see oracle/philox_oracle.c)
+    const double pd = (double)p;
+    return pd >= 1.0 ? 0.0f : 1.0f / (float)(1.0 - pd);
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+size_t elem_size(int dtype) { return dtype == MCGMIL_BF16 ? 2 : 4; }
+
+// Largest row tile whose masked feature tile fits the 128 KiB LDS budget.
+int pick_bm(int dtype, int L) {
+    const size_t es = elem_size(dtype);
+    if (dtype == MCGMIL_BF16) return (size_t)128 * L * es <= 131072 ? 128 : 32;
+    return (size_t)64 * L * es <= 131072 ? 64 : 16;
+}
+
+int validate_sizes(const mcgmil_args* a) {
+    if (!a) return fail(MCGMIL_E_INVALID, "args is NULL");
+    if (a->L <= 0 || a->L % 32 != 0) return fail(MCGMIL_E_UNSUPPORTED, "L must be a positive multiple of 32");
+    if (a->L > 2048) return fail(MCGMIL_E_UNSUPPORTED, "L > 2048 is not built");
+    if (a->D <= 0 || a->D % 16 != 0) return fail(MCGMIL_E_UNSUPPORTED, "D must be a positive multiple of 16");
+    if (a->C < 1 || a->C > 4) return fail(MCGMIL_E_UNSUPPORTED, "num_classes C must be in 1..4");
+    if (!(a->G == 1 || a->G == a->C)) return fail(MCGMIL_E_INVALID, "G must be 1 (shared) or C (separate)");
+    if (a->h_dtype != MCGMIL_F32 && a->h_dtype != MCGMIL_BF16) return fail(MCGMIL_E_INVALID, "h_dtype must be MCGMIL_F32 or MCGMIL_BF16");
+    return MCGMIL_OK;
+}
+
+int validate_batch(const mcgmil_args* a) {
+    int rc = validate_sizes(a);
+    if (rc) return rc;
+    if (a->T < 1) return fail(MCGMIL_E_INVALID, "T (number of MC samples) must be >= 1");
+    if (a->num_bags < 1) return fail(MCGMIL_E_INVALID, "num_bags must be >= 1");
+    if (a->total_rows < 0) return fail(MCGMIL_E_INVALID, "total_rows must be >= 0");
+    if ((long long)a->T * a->total_rows > (1ll << 46)) return fail(MCGMIL_E_UNSUPPORTED, "T * total_rows too large");
+    if (a->total_rows > 0x7fffffffll) return fail(MCGMIL_E_UNSUPPORTED, "total_rows must fit int32");
+    if (!a->bag_offsets) return fail(MCGMIL_E_INVALID, "bag_offsets is NULL");
+    if (!(a->p_feat >= 0.f && a->p_feat <= 1.f) || !(a->p_att >= 0.f && a->p_att <= 1.f))
+        return fail(MCGMIL_E_INVALID, "dropout probabilities must be in [0, 1]");
+    return MCGMIL_OK;
+}
+
+struct Layout {
+    size_t packed_bytes;   // 0 when args->packed_w is supplied
+    size_t logits_off, zz_off, total;
+};
+
+size_t packed_bytes_for(const mcgmil_args* a) {
+    const size_t P = (size_t)a->G * (a->D / 16);
+    return (2 * P + 1) * (size_t)(a->L / 32) * 512 * elem_size(a->h_dtype);
+}
+
+Layout layout_for(const mcgmil_args* a) {
+    Layout l;
+    l.packed_bytes = a->packed_w ? 0 : align_up(packed_bytes_for(a), 256);
+    const size_t scores = align_up((size_t)a->T * a->total_rows * a->C * sizeof(float), 256);
+    l.logits_off = l.packed_bytes;
+    l.zz_off = l.logits_off + scores;
+    l.total = l.zz_off + scores;
+    return l;
+}
+
+int check_workspace(const mcgmil_args* a, const Layout& l) {
+    if (l.total > 0 && (!a->workspace || a->workspace_bytes < l.total))
+        return fail(MCGMIL_E_WORKSPACE, "workspace missing or smaller than mcgmil_workspace_size()");
+    if (((uintptr_t)a->workspace & 255u) != 0) return fail(MCGMIL_E_ALIGN, "workspace must be 256-byte aligned");
+    return MCGMIL_OK;
+}
+
+const void* packed_ptr(const mcgmil_args* a) {
+    return a->packed_w ? a->packed_w : a->workspace;
+}
+
+template <typename E, int BM, int PPW, int MAXC>
+int launch_gate(const mcgmil::GateParams& gp, hipStream_t s) {
+    auto* k = &mcgmil::gate_scores_kernel<E, BM, PPW, MAXC>;
+    const size_t lds = mcgmil::gate_lds_bytes<E, BM, MAXC>(gp.L);
+    // All scratch is dynamic LDS (> 64 KiB): raise this instantiation's cap once.
+    static std::once_flag once;
+    std::call_once(once, [&] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    const long long tiles = (gp.total_samples + BM - 1) / BM;
+    if (tiles == 0) return MCGMIL_OK;
+    hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(mcgmil::kGateThreads), lds, s, gp);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_scores_kernel launch");
+}
+
+template <typename E, int BM>
+int dispatch_gate_ppw(const mcgmil::GateParams& gp, hipStream_t s) {
+    const bool two = gp.P % (2 * mcgmil::kGateWaves) == 0;
+    if (gp.C <= 2) {
+        return two ? launch_gate<E, BM, 2, 2>(gp, s) : launch_gate<E, BM, 1, 2>(gp, s);
+    }
+    return two ? launch_gate<E, BM, 2, 4>(gp, s) : launch_gate<E, BM, 1, 4>(gp, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mcgmil_abi_version(void) { return MCGMIL_ABI_VERSION; }
+
+size_t mcgmil_args_size(void) { return sizeof(mcgmil_args); }
+
+const char* mcgmil_last_error(void) { return g_last_error.c_str(); }
+
+int mcgmil_packed_weights_size(const mcgmil_args* a, size_t* bytes) {
+    int rc = validate_sizes(a);
+    if (rc) return rc;
+    if (!bytes) return fail(MCGMIL_E_INVALID, "bytes is NULL");
+    *bytes = packed_bytes_for(a);
+    return MCGMIL_OK;
+}
+
+int mcgmil_workspace_size(const mcgmil_args* a, size_t* bytes) {
+    int rc = validate_batch(a);
+    if (rc) return rc;
+    if (!bytes) return fail(MCGMIL_E_INVALID, "bytes is NULL");
+    *bytes = layout_for(a).total;
+    return MCGMIL_OK;
+}
+
+int mcgmil_pack_weights(const mcgmil_args* a, void* packed, void* stream) {
+    int rc = validate_sizes(a);
+    if (rc) return rc;
+    if (!packed || !a->Wv || !a->Wu || !a->wk) return fail(MCGMIL_E_INVALID, "NULL weight or output pointer");
+    const int P = a->G * (a->D / 16);
+    const size_t total = (size_t)(2 * P + 1) * (a->L / 32) * 512;
+    const unsigned blocks = (unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (a->h_dtype == MCGMIL_BF16)
+        hipLaunchKernelGGL(mcgmil::pack_weights_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, a->Wv,
+                           a->Wu, a->wk, a->L, a->D, a->C, P, reinterpret_cast<__bf16*>(packed));
+    else
+        hipLaunchKernelGGL(mcgmil::pack_weights_kernel<float>, dim3(blocks), dim3(256), 0, s, a->Wv,
+                           a->Wu, a->wk, a->L, a->D, a->C, P, reinterpret_cast<float*>(packed));
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "pack_weights_kernel launch");
+}
+
+int mcgmil_gate_scores(const mcgmil_args* a, void* stream) {
+    int rc = validate_batch(a);
+    if (rc) return rc;
+    const Layout l = layout_for(a);
+    if ((rc = check_workspace(a, l))) return rc;
+    if (!a->H && a->total_rows > 0) return fail(MCGMIL_E_INVALID, "H is NULL");
+    if (!a->bv || !a->bu || !a->wa || !a->ba) return fail(MCGMIL_E_INVALID, "NULL bias / attention weight pointer");
+    if (a->ldh < a->L) return fail(MCGMIL_E_INVALID, "ldh must be >= L");
+    if (!aligned16(a->H) || (a->ldh * (long long)elem_size(a->h_dtype)) % 16 != 0)
+        return fail(MCGMIL_E_ALIGN, "H and its row stride must be 16-byte aligned");
+    if (!aligned16(a->bv) || !aligned16(a->bu) || !aligned16(a->wa))
+        return fail(MCGMIL_E_ALIGN, "bv, bu and wa must be 16-byte aligned");
+    if ((a->keep_feat == nullptr) != (a->keep_att == nullptr))
+        return fail(MCGMIL_E_INVALID, "replay mode needs both keep_feat and keep_att");
+    if (a->packed_w && !aligned16(a->packed_w)) return fail(MCGMIL_E_ALIGN, "packed_w must be 16-byte aligned");
+
+    mcgmil::GateParams gp;
+    gp.H = a->H;
+    gp.ldh = a->ldh;
+    gp.bag_off = a->bag_offsets;
+    gp.B = a->num_bags;
+    gp.T = a->T;
+    gp.L = a->L;
+    gp.D = a->D;
+    gp.C = a->C;
+    gp.G = a->G;
+    gp.P = a->G * (a->D / 16);
+    gp.total_samples = (long long)a->T * a->total_rows;
+    gp.Wp = packed_ptr(a);
+    gp.bv = a->bv;
+    gp.bu = a->bu;
+    gp.wa = a->wa;
+    gp.ba = a->ba;
+    gp.sf = dropout_scale(a->p_feat);
+    gp.sa = dropout_scale(a->p_att);
+    gp.thr_f = drop_threshold(a->p_feat);
+    gp.thr_a = drop_threshold(a->p_att);
+    gp.k0 = (uint32_t)a->seed;
+    gp.k1 = (uint32_t)(a->seed >> 32);
+    gp.bag_base = a->bag_id_base;
+    gp.t_base = a->t_base;
+    gp.bag_ids = a->bag_ids;
+    gp.keep_feat = a->keep_feat;
+    gp.keep_att = a->keep_att;
+    gp.logits = reinterpret_cast<float*>(static_cast<char*>(a->workspace) + l.logits_off);
+    gp.zz = reinterpret_cast<float*>(static_cast<char*>(a->workspace) + l.zz_off);
+
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int bm = pick_bm(a->h_dtype, a->L);
+    if (a->h_dtype == MCGMIL_BF16)
+        return bm == 128 ? dispatch_gate_ppw<__bf16, 128>(gp, s) : dispatch_gate_ppw<__bf16, 32>(gp, s);
+    return bm == 64 ? dispatch_gate_ppw<float, 64>(gp, s) : dispatch_gate_ppw<float, 16>(gp, s);
+}
+
+int mcgmil_softmax_pool(const mcgmil_args* a, void* stream) {
+    int rc = validate_batch(a);
+    if (rc) return rc;
+    const Layout l = layout_for(a);
+    if ((rc = check_workspace(a, l))) return rc;
+    if (!a->Y) return fail(MCGMIL_E_INVALID, "Y is NULL");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const float* logits = reinterpret_cast<const float*>(static_cast<const char*>(a->workspace) + l.logits_off);
+    const float* zz = reinterpret_cast<const float*>(static_cast<const char*>(a->workspace) + l.zz_off);
+    hipLaunchKernelGGL(mcgmil::softmax_pool_kernel, dim3(a->T, a->num_bags), dim3(256), 0, s,
+                       a->bag_offsets, a->T, a->C, logits, zz, a->Y, a->A);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "softmax_pool_kernel launch");
+}
+
+int mcgmil_bag_stats(const mcgmil_args* a, void* stream) {
+    int rc = validate_batch(a);
+    if (rc) return rc;
+    if (!a->A_mean && !a->A_var && !a->P_mean) return MCGMIL_OK;
+    if ((a->A_mean || a->A_var) && !a->A) return fail(MCGMIL_E_INVALID, "A_mean/A_var need the A output");
+    if (!a->Y) return fail(MCGMIL_E_INVALID, "Y is NULL");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(mcgmil::bag_stats_kernel, dim3(a->C, a->num_bags), dim3(256), 0, s,
+                       a->bag_offsets, a->T, a->C, a->A, a->Y, a->A_mean, a->A_var, a->P_mean);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "bag_stats_kernel launch");
+}
+
+int mcgmil_mcdo_forward(const mcgmil_args* a, void* stream) {
+    int rc = validate_batch(a);
+    if (rc) return rc;
+    const Layout l = layout_for(a);
+    if ((rc = check_workspace(a, l))) return rc;
+    if (!a->packed_w) {
+        if ((rc = mcgmil_pack_weights(a, a->workspace, stream))) return rc;
+    }
+    if ((rc = mcgmil_gate_scores(a, stream))) return rc;
+    if ((rc = mcgmil_softmax_pool(a, stream))) return rc;
+    return mcgmil_bag_stats(a, stream);
+}
+
+int mcgmil_feature_keep(const mcgmil_args* a, uint8_t* keep_feat, void* stream) {
+    int rc = validate_batch(a);
+    if (rc) return rc;
+    if (!keep_feat) return fail(MCGMIL_E_INVALID, "keep_feat is NULL");
+    const long long total = (long long)a->T * a->total_rows * (a->L / 8);
+    if (total == 0) return MCGMIL_OK;
+    const unsigned blocks = (unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+    hipLaunchKernelGGL(mcgmil::feature_keep_kernel, dim3(blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), a->bag_offsets, a->num_bags, a->T,
+                       a->L / 8, (long long)a->T * a->total_rows, (uint32_t)a->seed,
+                       (uint32_t)(a->seed >> 32), a->bag_id_base, a->bag_ids, a->t_base,
+                       drop_threshold(a->p_feat), keep_feat);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "feature_keep_kernel launch");
+}
+
+int mcgmil_attention_keep(const mcgmil_args* a, uint8_t* keep_att, void* stream) {
+    int rc = validate_batch(a);
+    if (rc) return rc;
+    if (!keep_att) return fail(MCGMIL_E_INVALID, "keep_att is NULL");
+    const long long total = (long long)a->T * a->C * a->total_rows;
+    if (total == 0) return MCGMIL_OK;
+    const unsigned blocks = (unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+    hipLaunchKernelGGL(mcgmil::attention_keep_kernel, dim3(blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), a->bag_offsets, a->num_bags, a->T,
+                       a->C, total, (uint32_t)a->seed, (uint32_t)(a->seed >> 32), a->bag_id_base,
+                       a->bag_ids, a->t_base, drop_threshold(a->p_att), keep_att);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "attention_keep_kernel launch");
+}
+
+}  // extern "C"

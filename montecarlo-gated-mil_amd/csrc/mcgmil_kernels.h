@@ -1,0 +1,449 @@
+#pragma once
+// MI355X (gfx950) kernels of the Monte-Carlo-dropout gated-attention MIL hot path.
+//
+// Reference: MultiHeadGatedAttentionMIL.mc_inference, xkuubix/MonteCarlo-Gated-MIL
+// model.py:279-316 (everything after feature extraction). One launch of gate_scores_kernel
+// runs ALL T dropout samples of ALL bags of a batch:
+//
+//   rows  = flattened (bag, t, n), T * sum(N_b) of them, BM per workgroup
+//   X     = H[n] (.) keepF[bag,t,n]                          (model.py:280-281, masks in-register)
+//   S     = X . [Wv_g ; Wu_g ; wk]^T   one MFMA GEMM per row tile (model.py:285-286 / 297-298, 313)
+//   s_c   = sum_d tanh(S_v*sf + bv) sigmoid(S_u*sf + bu) wa_c + ba_c   (model.py:287-290 / 299)
+//   s'_c  = s_c * keepA * sa                                  (model.py:291 / 301)
+//   z_c   = sf * S_k                                          (classifier folded into the GEMM)
+// softmax_pool_kernel then does A = softmax_n(s') and Y_c = sum_n A z_c (model.py:305-316,
+// using Y_c = (sum_n A_n H_drop[n]) . k_c = sum_n A_n (H_drop[n] . k_c)), and bag_stats_kernel
+// the callers' uncertainty reductions (infer.py:195,212-219; net_utils.py:207-208).
+#include "mcgmil_device.h"
+
+namespace mcgmil {
+
+struct GateParams {
+    const void* H;
+    long long ldh;
+    const int32_t* bag_off;
+    int B, T, L, D, C, G, P;       // P = G * D / 16 gate tile pairs
+    long long total_samples;       // T * total_rows
+    const void* Wp;                // packed weights (see pack_weights_kernel)
+    const float* bv;
+    const float* bu;
+    const float* wa;
+    const float* ba;
+    float sf, sa;                  // dropout scales 1/(1-p) (0 for p = 1)
+    uint32_t thr_f, thr_a;         // 16-bit drop thresholds
+    uint32_t k0, k1;               // Philox key = seed
+    uint32_t bag_base;
+    int t_base;
+    const uint32_t* bag_ids;       // per-bag Philox counters or nullptr (bag_base + b)
+    const uint8_t* keep_feat;      // replay masks (parity mode) or nullptr
+    const uint8_t* keep_att;
+    float* logits;                 // [T*total_rows, C]
+    float* zz;                     // [T*total_rows, C]
+};
+
+constexpr int kGateThreads = 512;  // 8 waves
+constexpr int kGateWaves = kGateThreads / kWave;
+
+constexpr int kRowInfo = 6;  // ints per row: hrow, t, n, bag, Nb, bag counter
+
+template <int BM>
+__host__ __device__ constexpr int gate_row_info_ints() { return kRowInfo * BM; }
+
+// Dynamic LDS of gate_scores_kernel: [X tile BM*L elems][red NW*MAXC*BM f32][zred MAXC*BM f32]
+// [row info 5*BM i32]. Every carve offset is a multiple of 16 bytes.
+template <typename E, int BM, int MAXC>
+__host__ __device__ constexpr size_t gate_lds_bytes(int L) {
+    return (size_t)BM * L * sizeof(E) + (size_t)kGateWaves * MAXC * BM * 4 + (size_t)MAXC * BM * 4 +
+           (size_t)gate_row_info_ints<BM>() * 4;
+}
+
+// ---------------------------------------------------------------------------------------
+// gate_scores_kernel: one workgroup = BM rows of the flattened (bag, t, n) space.
+//   phase 1: row table (bag, t, n) in LDS;
+//   phase 2: stage X = H (.) keep for the BM rows into LDS as MFMA B fragments
+//            (one Philox4x32-10 block = 8 keep decisions = one 8-element fragment chunk);
+//   phase 3: per pass, wave w computes gate tile pairs (V_q, U_q) for all BM rows with the
+//            weight fragments streamed from L2 (packed, one 16-B load per lane), and folds
+//            tanh*sigmoid*wa into per-lane partial scores; waves w < BM/16 also compute the
+//            classifier projection z for row tile w;
+//   phase 4: cross-wave reduction, bias, attention dropout, store s' and z.
+// ---------------------------------------------------------------------------------------
+template <typename E, int BM, int PPW, int MAXC>
+__global__ __launch_bounds__(kGateThreads) void gate_scores_kernel(const GateParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int RT = BM / 16;        // 16-row tiles per workgroup
+    constexpr int NJ = 2 * PPW;        // weight column tiles per wave per pass
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int L = p.L;
+    const int KS = L >> 5;             // 32-deep K steps
+    const int LC = L >> 3;             // 8-element chunks per row
+
+    E* Xs = reinterpret_cast<E*>(smem);
+    float* red = reinterpret_cast<float*>(smem + (size_t)BM * L * sizeof(E));
+    float* zred = red + kGateWaves * MAXC * BM;
+    int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);  // [r][kRowInfo]
+
+    const long long R0 = (long long)blockIdx.x * BM;
+
+    // ---- phase 1: row table ----
+    if (tid < BM) {
+        const long long R = R0 + tid;
+        int hrow = -1, t = 0, n = 0, bag = 0, Nb = 0;
+        if (R < p.total_samples) {
+            bag = find_bag(p.bag_off, p.B, p.T, R);
+            const int ob = p.bag_off[bag];
+            Nb = p.bag_off[bag + 1] - ob;
+            const long long local = R - (long long)p.T * ob;
+            t = (int)(local / Nb);
+            n = (int)(local - (long long)t * Nb);
+            hrow = ob + n;
+        }
+        int* ri = rinfo + kRowInfo * tid;
+        ri[0] = hrow; ri[1] = t; ri[2] = n; ri[3] = bag; ri[4] = Nb;
+        ri[5] = (int)(p.bag_ids ? p.bag_ids[bag] : p.bag_base + (uint32_t)bag);
+    }
+    __syncthreads();
+
+    // ---- phase 2: stage the masked feature tile ----
+    {
+        const E* H = reinterpret_cast<const E*>(p.H);
+        const int items = BM * LC;
+        for (int i = tid; i < items; i += kGateThreads) {
+            const int blk = i >> 6, slot = i & 63;
+            const int rt = blk / KS, ks = blk - rt * KS;
+            const int r = rt * 16 + (slot & 15);
+            const int kc = ks * 4 + (slot >> 4);
+            E* dst = Xs + ((size_t)blk * 64 + slot) * 8;
+            const int* ri = rinfo + kRowInfo * r;
+            const int hrow = ri[0];
+            if (hrow < 0) {
+                store_zero8(dst);
+                continue;
+            }
+            uint32_t kb;
+            if (p.keep_feat) {
+                kb = p.keep_feat[(size_t)(R0 + r) * LC + kc];
+            } else {
+                const uint4 o = philox4x32_10((uint32_t)kc, (uint32_t)ri[2],
+                                              (uint32_t)(p.t_base + ri[1]), (uint32_t)ri[5],
+                                              p.k0, p.k1);
+                kb = keep_byte(o, p.thr_f);
+            }
+            load_masked(H + (size_t)hrow * p.ldh + (size_t)kc * 8, kb, dst);
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 3: gate GEMM + fused epilogue ----
+    const E* Wp = reinterpret_cast<const E*>(p.Wp);
+    const int DB = p.D >> 4;                   // 16-wide d blocks per gate
+    const int pairs_per_pass = kGateWaves * PPW;
+    const int npass = (p.P + pairs_per_pass - 1) / pairs_per_pass;
+    const size_t tile_elems = (size_t)KS * 512;  // one packed 16-column tile
+    const int lgrp = lane >> 4;                 // 4-row group inside the 16x16 accumulator
+
+    float part[MAXC][RT];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) part[c][rt] = 0.f;
+    f32x4 zacc = {0.f, 0.f, 0.f, 0.f};
+    const bool zwave = wave < RT;
+
+    for (int pass = 0; pass < npass; ++pass) {
+        const int q0 = pass * pairs_per_pass + wave * PPW;
+        const bool active = q0 < p.P;
+        const bool doz = (pass == 0) && zwave;
+        if (!active && !doz) continue;
+
+        f32x4 acc[RT][NJ];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+        const E* wbase[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            int q = q0 + (j >> 1);
+            q = q < p.P ? q : p.P - 1;             // idle slots read a valid tile, unused
+            wbase[j] = Wp + (size_t)(2 * q + (j & 1)) * tile_elems + lane * 8;
+        }
+        const E* zbase = Wp + (size_t)(2 * p.P) * tile_elems + lane * 8;
+
+        Frag<E> wcur[NJ], wnxt[NJ];
+        Frag<E> zcur = zero_frag<E>(), znxt = zero_frag<E>();
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) wcur[j] = active ? load_frag(wbase[j]) : zero_frag<E>();
+        if (doz) zcur = load_frag(zbase);
+
+        for (int ks = 0; ks < KS; ++ks) {
+            if (ks + 1 < KS) {
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    if (active) wnxt[j] = load_frag(wbase[j] + (size_t)(ks + 1) * 512);
+                if (doz) znxt = load_frag(zbase + (size_t)(ks + 1) * 512);
+            }
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                const Frag<E> x = load_frag(Xs + ((size_t)(rt * KS + ks) * 64 + lane) * 8);
+                if (active) {
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) acc[rt][j] = mma(wcur[j], x, acc[rt][j]);
+                }
+                if (doz && rt == wave) zacc = mma(zcur, x, zacc);
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) wcur[j] = wnxt[j];
+            zcur = znxt;
+        }
+
+        if (!active) continue;
+        // epilogue: lane holds instance rt*16 + (lane & 15), d = db*16 + 4*lgrp + v
+#pragma unroll
+        for (int jp = 0; jp < PPW; ++jp) {
+            const int q = q0 + jp;
+            if (q >= p.P) break;
+            const int g = q / DB, db = q - g * DB;
+            const int d0 = db * 16 + 4 * lgrp;
+            const f32x4 bvv = *reinterpret_cast<const f32x4*>(p.bv + (size_t)g * p.D + d0);
+            const f32x4 buv = *reinterpret_cast<const f32x4*>(p.bu + (size_t)g * p.D + d0);
+            f32x4 coef[MAXC];
+#pragma unroll
+            for (int c = 0; c < MAXC; ++c) {
+                const bool use = (c < p.C) && (p.G == 1 || c == g);
+                // address stays inside wa[C, D] for every c; unused classes get 0
+                const f32x4 w = *reinterpret_cast<const f32x4*>(p.wa + (size_t)(use ? c : 0) * p.D + d0);
+                coef[c] = use ? w : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const float av = gate_tanh(acc[rt][2 * jp][v] * p.sf + bvv[v]);
+                    const float au = gate_sigmoid(acc[rt][2 * jp + 1][v] * p.sf + buv[v]);
+                    const float pr = av * au;
+#pragma unroll
+                    for (int c = 0; c < MAXC; ++c) part[c][rt] = fmaf(pr, coef[c][v], part[c][rt]);
+                }
+            }
+        }
+    }
+
+    // ---- phase 4: reductions, bias, attention dropout, stores ----
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            float v = part[c][rt];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            if (lane < 16) red[(wave * MAXC + c) * BM + rt * 16 + lane] = v;
+        }
+    if (zwave && lane < 16) {
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) zred[c * BM + wave * 16 + lane] = zacc[c];
+    }
+    __syncthreads();
+
+    for (int i = tid; i < BM * p.C; i += kGateThreads) {
+        const int c = i / BM, r = i - c * BM;
+        const int* ri = rinfo + kRowInfo * r;
+        if (ri[0] < 0) continue;
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < kGateWaves; ++w) s += red[(w * MAXC + c) * BM + r];
+        s += p.ba[c];
+        const int t = ri[1], n = ri[2], bag = ri[3], Nb = ri[4];
+        bool keep;
+        if (p.keep_att) {
+            const size_t abase = (size_t)p.T * p.C * (size_t)p.bag_off[bag];
+            keep = p.keep_att[abase + ((size_t)t * p.C + c) * Nb + n] != 0;
+        } else {
+            keep = attention_keep(p.k0, p.k1, (uint32_t)ri[5], (uint32_t)(p.t_base + t),
+                                  (uint32_t)c, (uint32_t)n, p.thr_a);
+        }
+        const size_t o = (size_t)(R0 + r) * p.C + c;
+        p.logits[o] = s * (keep ? p.sa : 0.f);
+        p.zz[o] = zred[c * BM + r] * p.sf;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// softmax_pool_kernel: one 256-thread block per (t, bag). A = softmax over the bag's
+// instances (model.py:305), Y_c = sum_n A z_c (model.py:308-316).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void softmax_pool_kernel(const int32_t* bag_off, int T, int C,
+                                                           const float* logits, const float* zz,
+                                                           float* Y, float* A) {
+    __shared__ float sred[2][4];
+    const int t = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ob = bag_off[b];
+    const int Nb = bag_off[b + 1] - ob;
+    float* Yo = Y + ((size_t)b * T + t) * C;
+    if (Nb == 0) {
+        if (tid < C) Yo[tid] = 0.f;
+        return;
+    }
+    const size_t R0 = (size_t)T * ob + (size_t)t * Nb;
+    const size_t abase = (size_t)T * C * ob + (size_t)t * C * Nb;
+    for (int c = 0; c < C; ++c) {
+        float m = -INFINITY;
+        for (int n = tid; n < Nb; n += 256) m = fmaxf(m, logits[(R0 + n) * C + c]);
+        m = wave_max(m);
+        if (lane == 0) sred[0][wave] = m;
+        __syncthreads();
+        m = fmaxf(fmaxf(sred[0][0], sred[0][1]), fmaxf(sred[0][2], sred[0][3]));
+        __syncthreads();
+        float s = 0.f, y = 0.f;
+        for (int n = tid; n < Nb; n += 256) {
+            const size_t o = (R0 + n) * C + c;
+            const float e = expf(logits[o] - m);
+            s += e;
+            y = fmaf(e, zz[o], y);
+        }
+        s = wave_sum(s);
+        y = wave_sum(y);
+        if (lane == 0) { sred[0][wave] = s; sred[1][wave] = y; }
+        __syncthreads();
+        s = (sred[0][0] + sred[0][1]) + (sred[0][2] + sred[0][3]);
+        y = (sred[1][0] + sred[1][1]) + (sred[1][2] + sred[1][3]);
+        __syncthreads();
+        const float inv = 1.0f / s;
+        if (A) {
+            float* Ao = A + abase + (size_t)c * Nb;
+            for (int n = tid; n < Nb; n += 256) Ao[n] = expf(logits[(R0 + n) * C + c] - m) * inv;
+        }
+        if (tid == 0) Yo[c] = y * inv;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// bag_stats_kernel: one 256-thread block per (class, bag). Mean and unbiased variance of the
+// attention over the T passes (infer.py:216-219: torch .mean/.std, var = std^2) and the mean
+// class probability (infer.py:195 softmax over classes; net_utils.py:207-208 mean over T).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bag_stats_kernel(const int32_t* bag_off, int T, int C,
+                                                        const float* A, const float* Y,
+                                                        float* A_mean, float* A_var, float* P_mean) {
+    __shared__ double sred[4];
+    const int c = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ob = bag_off[b];
+    const int Nb = bag_off[b + 1] - ob;
+    if (A && (A_mean || A_var)) {
+        const size_t abase = (size_t)T * C * ob + (size_t)c * Nb;
+        const size_t sbase = (size_t)C * ob + (size_t)c * Nb;
+        for (int n = tid; n < Nb; n += 256) {
+            double s = 0.0;
+            for (int t = 0; t < T; ++t) s += A[abase + (size_t)t * C * Nb + n];
+            const double mean = s / T;
+            double ss = 0.0;
+            for (int t = 0; t < T; ++t) {
+                const double d = (double)A[abase + (size_t)t * C * Nb + n] - mean;
+                ss += d * d;
+            }
+            if (A_mean) A_mean[sbase + n] = (float)mean;
+            if (A_var) A_var[sbase + n] = T > 1 ? (float)(ss / (T - 1)) : NAN;
+        }
+    }
+    if (P_mean) {
+        double acc = 0.0;
+        for (int t = tid; t < T; t += 256) {
+            const float* y = Y + ((size_t)b * T + t) * C;
+            float m = y[0];
+            for (int k = 1; k < C; ++k) m = fmaxf(m, y[k]);
+            float s = 0.f;
+            for (int k = 0; k < C; ++k) s += expf(y[k] - m);
+            acc += (double)(expf(y[c] - m) / s);
+        }
+        acc = wave_sum_d(acc);
+        if (lane == 0) sred[wave] = acc;
+        __syncthreads();
+        if (tid == 0) P_mean[(size_t)b * C + c] = (float)(((sred[0] + sred[1]) + (sred[2] + sred[3])) / T);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// pack_weights_kernel: fp32 nn.Linear weights -> MFMA A-operand tiles of dtype E.
+// Tile 2q / 2q+1 = V / U columns d = 16*db .. 16*db+15 of gate g (q = g*D/16 + db);
+// tile 2P = classifier rows (c < C), zero-padded to 16. Each tile is KS blocks of
+// 64 lanes x 8 elements: lane l, element j = W[col l & 15][k = 32*ks + 8*(l >> 4) + j].
+// ---------------------------------------------------------------------------------------
+template <typename E>
+__global__ void pack_weights_kernel(const float* Wv, const float* Wu, const float* wk, int L, int D,
+                                    int C, int P, E* out) {
+    const int KS = L >> 5;
+    const size_t total = (size_t)(2 * P + 1) * KS * 512;
+    const int DB = D >> 4;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int j = (int)(i & 7);
+        const int lane = (int)((i >> 3) & 63);
+        const size_t blk = i >> 9;
+        const int ks = (int)(blk % KS);
+        const int tile = (int)(blk / KS);
+        const int col = lane & 15;
+        const int k = ks * 32 + 8 * (lane >> 4) + j;
+        float v;
+        if (tile < 2 * P) {
+            const int q = tile >> 1;
+            const int g = q / DB, db = q - g * DB;
+            const float* W = (tile & 1) ? Wu : Wv;
+            v = W[((size_t)g * D + db * 16 + col) * L + k];
+        } else {
+            v = col < C ? wk[(size_t)col * L + k] : 0.f;
+        }
+        out[i] = static_cast<E>(v);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Mask materialisation (parity tests): the exact decisions gate_scores_kernel draws.
+// ---------------------------------------------------------------------------------------
+__global__ void feature_keep_kernel(const int32_t* bag_off, int B, int T, int LC,
+                                    long long total_samples, uint32_t k0, uint32_t k1,
+                                    uint32_t bag_base, const uint32_t* bag_ids, int t_base,
+                                    uint32_t thr, uint8_t* out) {
+    const long long total = total_samples * LC;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long R = i / LC;
+        const int kc = (int)(i - R * LC);
+        const int bag = find_bag(bag_off, B, T, R);
+        const int ob = bag_off[bag];
+        const int Nb = bag_off[bag + 1] - ob;
+        const long long local = R - (long long)T * ob;
+        const int t = (int)(local / Nb);
+        const int n = (int)(local - (long long)t * Nb);
+        const uint32_t bagc = bag_ids ? bag_ids[bag] : bag_base + (uint32_t)bag;
+        const uint4 o = philox4x32_10((uint32_t)kc, (uint32_t)n, (uint32_t)(t_base + t), bagc,
+                                      k0, k1);
+        out[i] = (uint8_t)keep_byte(o, thr);
+    }
+}
+
+__global__ void attention_keep_kernel(const int32_t* bag_off, int B, int T, int C,
+                                      long long total, uint32_t k0, uint32_t k1,
+                                      uint32_t bag_base, const uint32_t* bag_ids, int t_base,
+                                      uint32_t thr, uint8_t* out) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int bag = find_bag(bag_off, B, (long long)T * C, i);
+        const int ob = bag_off[bag];
+        const int Nb = bag_off[bag + 1] - ob;
+        const long long local = i - (long long)T * C * ob;
+        const int t = (int)(local / ((long long)C * Nb));
+        const long long rem = local - (long long)t * C * Nb;
+        const int c = (int)(rem / Nb);
+        const int n = (int)(rem - (long long)c * Nb);
+        const uint32_t bagc = bag_ids ? bag_ids[bag] : bag_base + (uint32_t)bag;
+        out[i] = attention_keep(k0, k1, bagc, (uint32_t)(t_base + t), (uint32_t)c, (uint32_t)n,
+                                thr) ? 1 : 0;
+    }
+}
+
+}  // namespace mcgmil

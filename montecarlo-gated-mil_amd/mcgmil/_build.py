@@ -1,0 +1,42 @@
+"""Build the in-tree HIP library libmcgmil.so for gfx950 (hipcc cross-compiles without a GPU).
+
+The .so is written next to this file (git-ignored) so it travels to the GPU box with the repo
+snapshot and is what the drop-in module loads.
+"""
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(ROOT, "csrc")
+INCLUDE = os.path.join(os.path.dirname(ROOT), "include")
+LIB = os.path.join(PKG, "libmcgmil.so")
+SOURCES = ["mcgmil.hip"]
+DEPS = ["mcgmil.hip", "mcgmil_kernels.h", "mcgmil_device.h"]
+ARCH = os.environ.get("MCGMIL_OFFLOAD_ARCH", "gfx950")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, d) for d in DEPS] + [os.path.join(INCLUDE, "mcgmil.h")]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
+    tmp = LIB + ".tmp"
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall",
+           "-Werror", f"-I{INCLUDE}", "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

@@ -1,0 +1,97 @@
+"""ctypes binding of the C ABI in include/mcgmil.h (libmcgmil.so, built for gfx950).
+
+torch is imported first on purpose: torch ships the HIP runtime (SONAME libamdhip64.so.7), and
+the library's NEEDED entry then resolves to that already-loaded copy, so the kernels run on
+torch's device context and streams.
+
+There is no fallback: if the library is missing or fails to load, every call raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before the library)
+
+from . import _build
+
+MCGMIL_F32 = 0
+MCGMIL_BF16 = 1
+
+EXPORTED = (
+    "mcgmil_abi_version", "mcgmil_args_size", "mcgmil_last_error", "mcgmil_workspace_size",
+    "mcgmil_packed_weights_size", "mcgmil_pack_weights", "mcgmil_mcdo_forward",
+    "mcgmil_gate_scores", "mcgmil_softmax_pool", "mcgmil_bag_stats", "mcgmil_feature_keep",
+    "mcgmil_attention_keep",
+)
+
+_vp = ctypes.c_void_p
+
+
+class Args(ctypes.Structure):
+    """Mirror of struct mcgmil_args (include/mcgmil.h); field order and types must match."""
+    _fields_ = [
+        ("L", ctypes.c_int32), ("D", ctypes.c_int32), ("C", ctypes.c_int32),
+        ("G", ctypes.c_int32), ("T", ctypes.c_int32), ("num_bags", ctypes.c_int32),
+        ("total_rows", ctypes.c_int64),
+        ("h_dtype", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+        ("H", _vp), ("ldh", ctypes.c_int64), ("bag_offsets", _vp),
+        ("Wv", _vp), ("bv", _vp), ("Wu", _vp), ("bu", _vp), ("wa", _vp), ("ba", _vp),
+        ("wk", _vp), ("packed_w", _vp),
+        ("p_feat", ctypes.c_float), ("p_att", ctypes.c_float), ("seed", ctypes.c_uint64),
+        ("bag_id_base", ctypes.c_uint32), ("t_base", ctypes.c_int32), ("bag_ids", _vp),
+        ("keep_feat", _vp), ("keep_att", _vp),
+        ("Y", _vp), ("A", _vp), ("A_mean", _vp), ("A_var", _vp), ("P_mean", _vp),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
+class MCGMILError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def load():
+    """Load libmcgmil.so (raises if it was not built -- there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not os.path.exists(path):
+        raise MCGMILError(f"MI355X extension not built: {path} is missing "
+                          "(run __graft_entry__.build() or python -m mcgmil._build)")
+    L = ctypes.CDLL(path)
+    pa = ctypes.POINTER(Args)
+    L.mcgmil_abi_version.restype = ctypes.c_int
+    L.mcgmil_args_size.restype = ctypes.c_size_t
+    L.mcgmil_last_error.restype = ctypes.c_char_p
+    for name in ("mcgmil_workspace_size", "mcgmil_packed_weights_size"):
+        f = getattr(L, name)
+        f.argtypes = [pa, ctypes.POINTER(ctypes.c_size_t)]
+        f.restype = ctypes.c_int
+    L.mcgmil_pack_weights.argtypes = [pa, _vp, _vp]
+    L.mcgmil_pack_weights.restype = ctypes.c_int
+    for name in ("mcgmil_mcdo_forward", "mcgmil_gate_scores", "mcgmil_softmax_pool",
+                 "mcgmil_bag_stats"):
+        f = getattr(L, name)
+        f.argtypes = [pa, _vp]
+        f.restype = ctypes.c_int
+    for name in ("mcgmil_feature_keep", "mcgmil_attention_keep"):
+        f = getattr(L, name)
+        f.argtypes = [pa, _vp, _vp]
+        f.restype = ctypes.c_int
+    if L.mcgmil_args_size() != ctypes.sizeof(Args):
+        raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_args)={L.mcgmil_args_size()} but the "
+                          f"ctypes mirror is {ctypes.sizeof(Args)} bytes")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().mcgmil_last_error().decode(errors="replace")
+        raise MCGMILError(f"{what} failed ({rc}): {msg}")

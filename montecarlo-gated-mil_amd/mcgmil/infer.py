@@ -1,0 +1,56 @@
+"""MCDO inference driver -- the build's counterpart of the reference callers of mc_inference
+(infer.py:187-219, net_utils.py:195-210), minus neptune, DICOM I/O and plotting.
+
+Runs a whole list of bags (extracted features) through ONE varlen kernel launch and returns,
+per bag, what the reference computes from (Y, A):
+  probs  = softmax(Y, dim=-1)                          infer.py:195 / net_utils.py:207
+  prob_mean, prediction = mean over passes, argmax     net_utils.py:208-210
+  positive-class mean/median/std/IQR/min/max           infer.py:47-54
+  mean entropy  -sum p log(p + 1e-10)                  infer.py:56-57
+  attention mean / unbiased variance over passes       infer.py:216-219 (per instance; the
+                                                       reference maps them onto the image)
+"""
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import ops
+
+
+def mc_predict_bags(model, bags: Sequence[torch.Tensor], T: int = 50, seed: Optional[int] = None,
+                    bag_ids: Optional[Sequence[int]] = None) -> List[dict]:
+    """bags: list of feature matrices H_b [N_b, L] on one HIP device."""
+    device = model._check_device(bags[0].device)
+    if seed is None:
+        seed = int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
+    sizes = [int(h.shape[0]) for h in bags]
+    H = torch.cat([h.reshape(-1, model.L) for h in bags]).to(model.compute_dtype).contiguous()
+    offs = ops.bag_offsets_tensor(sizes, device)
+    ids = None
+    if bag_ids is not None:
+        ids = torch.as_tensor(list(bag_ids), dtype=torch.int64).to(torch.int32).to(device)
+    head, packed = model.head_tensors(device)
+    pf, pa = model.feature_dropout.p, model.attention_dropouts[0].p
+    with torch.no_grad():
+        out = ops.mcdo_forward(H, offs, head, T, p_feat=pf, p_att=pa, seed=seed, packed=packed,
+                               return_stats=True, bag_ids=ids)
+    C = model.num_classes
+    Am = ops.split_bags(out["A_mean"], sizes, C)
+    Av = ops.split_bags(out["A_var"], sizes, C)
+    res = []
+    for b, n in enumerate(sizes):
+        Y = out["Y"][b]                                   # [T, C]
+        probs = torch.softmax(Y, dim=-1)
+        pos = probs[:, -1]
+        q = torch.quantile(pos, torch.tensor([0.25, 0.5, 0.75], device=pos.device))
+        ent = -(probs * torch.log(probs + 1e-10)).sum(-1)
+        res.append({
+            "Y": Y, "probs": probs, "prob_mean": out["P_mean"][b],
+            "prediction": int(torch.argmax(out["P_mean"][b])),
+            "pos_mean": float(pos.mean()), "pos_median": float(q[1]),
+            "pos_std": float(pos.std(unbiased=False)), "pos_iqr": float(q[2] - q[0]),
+            "pos_min": float(pos.min()), "pos_max": float(pos.max()),
+            "mean_entropy": float(ent.mean()),
+            "A_mean": Am[b].view(C, n), "A_var": Av[b].view(C, n),
+        })
+    return res

@@ -1,0 +1,42 @@
+#!/bin/bash
+# One gpurun session: smoke -> GPU parity tests -> bench -> rocprofv3 kernel stats.
+# Each GPU step has its own time limit. A plain failure (exit 1: a failed assertion) lets the
+# next step run; any other non-zero exit (fault/abort/segfault/timeout) ends the script.
+# Usage: bash scripts/gpu_check.sh [tag] [steps...]   (steps: smoke tests bench prof)
+set -u
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-smoke tests bench prof}
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+run() {  # name seconds cmd...
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name (limit ${secs}s): $*"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    tail -n 25 "$OUT/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+        echo "== stopping: $name exited with $rc"
+        exit $rc
+    fi
+    return 0
+}
+
+for s in $STEPS; do
+    case $s in
+        smoke) run smoke 420 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
+        tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+        bench) run bench 600 python bench.py ;;
+        prof)
+            rm -rf "$OUT/prof_$TAG"
+            run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run \
+                --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
+            find "$OUT/prof_$TAG" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_$TAG.csv" \;
+            ;;
+    esac
+done
+echo "== done"

@@ -1,0 +1,103 @@
+"""The C ABI library (CPU-side checks only: no kernel launches without a GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "mcgmil.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(mcgmil_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_entry_points():
+    fns = declared_functions()
+    for f in ("mcgmil_mcdo_forward", "mcgmil_workspace_size", "mcgmil_pack_weights",
+              "mcgmil_last_error", "mcgmil_feature_keep", "mcgmil_attention_keep"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol(hip_lib):
+    from mcgmil import _lib
+    for f in declared_functions():
+        assert hasattr(hip_lib, f), f
+    assert set(declared_functions()) == set(_lib.EXPORTED)
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.lib_path()], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (mcgmil_\w+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_library_targets_gfx950(hip_lib):
+    from mcgmil import _lib
+    data = open(_lib.lib_path(), "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data   # the embedded offload bundle's target
+
+
+def test_args_struct_matches_binding(hip_lib):
+    from mcgmil import _lib
+    assert hip_lib.mcgmil_abi_version() == 1
+    assert hip_lib.mcgmil_args_size() == ctypes.sizeof(_lib.Args)
+
+
+def _args(**kw):
+    from mcgmil import _lib
+    a = _lib.Args()
+    a.L, a.D, a.C, a.G, a.T, a.num_bags, a.total_rows = 512, 128, 2, 2, 100, 1, 2048
+    a.h_dtype = _lib.MCGMIL_BF16
+    a.bag_offsets = ctypes.c_void_p(0x1000)
+    a.p_feat = a.p_att = 0.1
+    for k, v in kw.items():
+        setattr(a, k, v)
+    return a
+
+
+def _ws(hip_lib, a):
+    n = ctypes.c_size_t()
+    rc = hip_lib.mcgmil_workspace_size(ctypes.byref(a), ctypes.byref(n))
+    return rc, n.value
+
+
+def test_workspace_size_formula(hip_lib):
+    rc, n = _ws(hip_lib, _args())
+    assert rc == 0
+    packed = (2 * 16 + 1) * 16 * 512 * 2                     # (2P+1) tiles x KS x 512 x bf16
+    scores = 100 * 2048 * 2 * 4
+    assert n == ((packed + 255) // 256) * 256 + 2 * scores
+    rc, n2 = _ws(hip_lib, _args(packed_w=ctypes.c_void_p(0x2000)))
+    assert rc == 0 and n2 == 2 * scores
+
+
+@pytest.mark.parametrize("field,value,code", [
+    ("L", 500, -2), ("L", 4096, -2), ("D", 100, -2), ("C", 5, -2), ("C", 0, -2), ("G", 3, -1),
+    ("T", 0, -1), ("num_bags", 0, -1), ("p_feat", 1.5, -1), ("p_att", -0.1, -1),
+    ("h_dtype", 7, -1), ("bag_offsets", None, -1), ("total_rows", -1, -1),
+])
+def test_validation_errors(hip_lib, field, value, code):
+    rc, _ = _ws(hip_lib, _args(**{field: value}))
+    assert rc == code
+    assert len(hip_lib.mcgmil_last_error()) > 0
+
+
+def test_forward_rejects_missing_workspace(hip_lib):
+    a = _args()
+    rc = hip_lib.mcgmil_mcdo_forward(ctypes.byref(a), None)
+    assert rc == -4
+    assert b"workspace" in hip_lib.mcgmil_last_error()
+
+
+def test_gate_rejects_misaligned_H(hip_lib):
+    a = _args(packed_w=ctypes.c_void_p(0x2000))
+    rc, n = _ws(hip_lib, a)
+    a.workspace, a.workspace_bytes = ctypes.c_void_p(0x10000), n
+    a.H, a.ldh = ctypes.c_void_p(0x3002), 512
+    a.bv = a.bu = a.wa = a.ba = ctypes.c_void_p(0x4000)
+    assert hip_lib.mcgmil_gate_scores(ctypes.byref(a), None) == -3
+    a.H, a.ldh = ctypes.c_void_p(0x3000), 509
+    assert hip_lib.mcgmil_gate_scores(ctypes.byref(a), None) == -1  # ldh < L

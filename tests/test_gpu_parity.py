@@ -1,0 +1,313 @@
+"""MI355X parity: the HIP kernels (through the C ABI) against the reference's golden outputs and
+the CPU oracle. Tolerances from SURVEY.md §8(d), nrel = max|d| / max|ref|:
+  fp32           : A nrel <= 1e-5, Y abs <= 1e-5, A_mean nrel <= 1e-5 (and abs <= 1e-4),
+                   A_var nrel <= 1e-4, P_mean abs <= 1e-5
+  bf16 kernel vs the bf16-rounded-input reference: the fp32 bounds x 10
+  bf16 kernel vs the pure fp32 reference: A_mean nrel <= 5e-3, A_var nrel <= 2e-2,
+                   Y abs <= 5e-3, P_mean abs <= 1e-3
+Masks are bit-exact by construction (the kernel's Philox == oracle/philox_oracle.c), checked
+directly in test_masks_bit_exact."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import GOLDEN, Case, names, nrel
+from oracle import mcdo_ref, philox, synthetic
+
+pytestmark = pytest.mark.gpu
+
+TOL32 = dict(A=1e-5, Y=1e-5, A_mean=1e-5, A_var=1e-4, P_mean=1e-5)
+TOL_BF16_IN = {k: 10 * v for k, v in TOL32.items()}
+TOL_BF16_VS_FP32 = dict(A=5e-3, Y=5e-3, A_mean=5e-3, A_var=2e-2, P_mean=1e-3)
+
+MC_CASES = [n for n in names() if not n.startswith("forward") and not n.startswith("serial")]
+FP32_CASES = [n for n in MC_CASES if "bf16in" not in n]
+BF16_CASES = [n for n in MC_CASES if "bf16in" in n]
+
+
+def head_on(arrays, dev):
+    from mcgmil.ops import HeadTensors
+    return HeadTensors(*[torch.from_numpy(np.ascontiguousarray(arrays[k])).to(dev)
+                         for k in HeadTensors._fields])
+
+
+def run(case, dev, dtype, replay=False, H=None):
+    from mcgmil import ops
+    Hn, _, arrays = case.inputs()
+    Hn = Hn if H is None else H
+    Ht = torch.from_numpy(Hn).to(dev).to(dtype).contiguous()
+    offs = ops.bag_offsets_tensor([case.N], dev)
+    kw = {}
+    if replay:
+        kF, kA = case.masks()
+        kw["keep_feat"] = torch.from_numpy(philox.pack_feature_bits(kF).reshape(case.T * case.N, -1)).to(dev)
+        kw["keep_att"] = torch.from_numpy(kA.astype(np.uint8).reshape(-1)).to(dev)
+    out = ops.mcdo_forward(Ht, offs, head_on(arrays, dev), case.T, p_feat=case.p_f,
+                           p_att=case.p_a, seed=case.mask_seed, bag_id_base=case.bag_ctr,
+                           return_stats=True, **kw)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items()}
+
+
+def compare(case, out, tol):
+    T, C, N = case.T, case.C, case.N
+    Y = out["Y"][0]                                     # [T, C]
+    A = out["A"].reshape(T, C, N)
+    ref_Y = case.z["Y"][:, 0]
+    np.testing.assert_allclose(Y, ref_Y, rtol=0, atol=tol["Y"])
+    if "A" in case.z:
+        assert nrel(A, case.z["A"][:, 0]) <= tol["A"]
+    else:
+        assert nrel(A[0], case.z["A_first"][0]) <= tol["A"]
+        assert nrel(A[-1], case.z["A_last"][0]) <= tol["A"]
+    Am = out["A_mean"].reshape(C, N)
+    assert nrel(Am, case.z["A_mean"][0]) <= tol["A_mean"]
+    assert np.max(np.abs(Am - case.z["A_mean"][0])) <= 1e-4        # the north-star bound
+    Av = out["A_var"].reshape(C, N)
+    if T > 1:
+        assert nrel(Av, case.z["A_var"][0]) <= tol["A_var"]
+        assert np.max(np.abs(Av - case.z["A_var"][0])) <= 1e-4
+    else:
+        assert np.isnan(Av).all()
+    np.testing.assert_allclose(out["P_mean"][0], case.z["P_mean"], rtol=0, atol=tol["P_mean"])
+    np.testing.assert_allclose(A.sum(-1), 1.0, atol=2e-5)
+
+
+# ------------------------------------------------------------------ masks
+def test_masks_bit_exact(cuda):
+    from mcgmil import ops
+    sizes = [5, 64, 0, 37, 130]
+    T, L, C, seed, base = 6, 512, 2, 0xDEADBEEF12345, 40
+    offs = ops.bag_offsets_tensor(sizes, cuda)
+    R = sum(sizes)
+    kf = ops.feature_keep(offs, R, T, L, 0.1, seed, bag_id_base=base, t_base=3).cpu().numpy()
+    ka = ops.attention_keep(offs, R, T, C, 0.3, seed, bag_id_base=base, t_base=3).cpu().numpy()
+    rf = ra = 0
+    for b, n in enumerate(sizes):
+        want_f = philox.feature_keep_bits(seed, base + b, T, n, L, 0.1, t0=3).reshape(T * n, -1)
+        want_a = philox.attention_keep(seed, base + b, T, C, n, 0.3, t0=3).astype(np.uint8).reshape(-1)
+        assert np.array_equal(kf[rf:rf + T * n], want_f), b
+        assert np.array_equal(ka[ra:ra + T * C * n], want_a), b
+        rf += T * n
+        ra += T * C * n
+    ids = torch.tensor([9, 1000, 3, 77, 5], dtype=torch.int32, device=cuda)
+    kf2 = ops.feature_keep(offs, R, T, L, 0.1, seed, bag_ids=ids).cpu().numpy()
+    want = philox.feature_keep_bits(seed, 77, T, 37, L, 0.1).reshape(T * 37, -1)
+    o = T * (5 + 64)
+    assert np.array_equal(kf2[o:o + T * 37], want)
+
+
+# ------------------------------------------------------------------ golden parity
+@pytest.mark.parametrize("name", FP32_CASES)
+def test_fp32_replay_matches_reference(cuda, name):
+    case = Case(name)
+    compare(case, run(case, cuda, torch.float32, replay=True), TOL32)
+
+
+@pytest.mark.parametrize("name", FP32_CASES)
+def test_fp32_philox_matches_reference(cuda, name):
+    case = Case(name)
+    compare(case, run(case, cuda, torch.float32), TOL32)
+
+
+@pytest.mark.parametrize("name", BF16_CASES)
+def test_bf16_matches_bf16_input_reference(cuda, name):
+    case = Case(name)
+    compare(case, run(case, cuda, torch.bfloat16), TOL_BF16_IN)
+
+
+def test_bf16_drift_vs_fp32_reference(cuda):
+    case = Case("cfg3_N2048_T100_sep")
+    compare(case, run(case, cuda, torch.bfloat16), TOL_BF16_VS_FP32)
+
+
+@pytest.mark.parametrize("name", ["small_N64_T4_sep", "edge_N37_T5_shared", "cfg2_N512_T30_sep"])
+def test_bf16_replay_matches_oracle(cuda, name):
+    case = Case(name)
+    Hn, sd, _ = case.inputs()
+    Hb = synthetic.bf16_round(Hn)
+    arr = synthetic.head_arrays(synthetic.round_state_dict_bf16(sd), case.C, case.shared)
+    kF, kA = case.masks()
+    Y, A = mcdo_ref.mc_inference(Hb, mcdo_ref.HeadParams(arr), kF, kA, case.p_f, case.p_a)
+    out = run(case, cuda, torch.bfloat16, replay=True, H=Hn)
+    np.testing.assert_allclose(out["Y"][0], Y[:, 0].numpy(), atol=TOL_BF16_IN["Y"])
+    assert nrel(out["A"].reshape(case.T, case.C, case.N), A[:, 0].numpy()) <= TOL_BF16_IN["A"]
+
+
+# ------------------------------------------------------------------ batches
+def test_varlen_batch_matches_per_bag_oracle(cuda):
+    """Several bags (incl. N=1, an empty bag, odd sizes) in ONE launch == per-bag oracle."""
+    from mcgmil import ops
+    sizes = [64, 1, 0, 37, 300, 128]
+    T, C, L, D, seed, base = 5, 2, 512, 128, 77, 11
+    sd = synthetic.head_state_dict(3, L=L, D=D, C=C, shared=False)
+    arrays = synthetic.head_arrays(sd, C, False)
+    Hs = [synthetic.bag_features(100 + b, n, L) for b, n in enumerate(sizes)]
+    H = torch.from_numpy(np.concatenate(Hs)).to(cuda)
+    offs = ops.bag_offsets_tensor(sizes, cuda)
+    out = ops.mcdo_forward(H, offs, head_on(arrays, cuda), T, p_feat=0.1, p_att=0.1, seed=seed,
+                           bag_id_base=base, return_stats=True)
+    Y = out["Y"].cpu().numpy()
+    A = ops.split_bags(out["A"].cpu(), sizes, T * C)
+    Am = ops.split_bags(out["A_mean"].cpu(), sizes, C)
+    prm = mcdo_ref.HeadParams(arrays)
+    for b, n in enumerate(sizes):
+        if n == 0:
+            assert np.all(Y[b] == 0)
+            continue
+        kF, kA = mcdo_ref.masks_for_bag(seed, base + b, T, n, L, C, 0.1, 0.1)
+        Yr, Ar = mcdo_ref.mc_inference(Hs[b], prm, kF, kA, 0.1, 0.1)
+        np.testing.assert_allclose(Y[b], Yr[:, 0].numpy(), atol=1e-5)
+        assert nrel(A[b].numpy().reshape(T, C, n), Ar[:, 0].numpy()) <= 1e-5
+        assert nrel(Am[b].numpy().reshape(C, n), Ar[:, 0].mean(0).numpy()) <= 1e-5
+
+
+def test_shard_with_bag_ids_is_bitwise_rank_independent(cuda):
+    """A subset of the batch run with its global bag ids reproduces the full batch bit for bit
+    (what makes 1/2/4/8-GPU sharding results identical)."""
+    from mcgmil import ops
+    sizes = [200, 50, 333, 17, 512]
+    T, C, L = 8, 2, 512
+    arrays = synthetic.head_arrays(synthetic.head_state_dict(4, C=C, shared=True), C, True)
+    head = head_on(arrays, cuda)
+    Hs = [torch.from_numpy(synthetic.bag_features(200 + b, n)).to(cuda).bfloat16() for b, n in enumerate(sizes)]
+    full = ops.mcdo_forward(torch.cat(Hs), ops.bag_offsets_tensor(sizes, cuda), head, T,
+                            p_feat=0.1, p_att=0.1, seed=5)
+    sub = [4, 1, 3]
+    ids = torch.tensor(sub, dtype=torch.int32, device=cuda)
+    part = ops.mcdo_forward(torch.cat([Hs[i] for i in sub]),
+                            ops.bag_offsets_tensor([sizes[i] for i in sub], cuda), head, T,
+                            p_feat=0.1, p_att=0.1, seed=5, bag_ids=ids)
+    assert torch.equal(part["Y"], full["Y"][sub])
+    Af = ops.split_bags(full["A"], sizes, T * C)
+    Ap = ops.split_bags(part["A"], [sizes[i] for i in sub], T * C)
+    for j, i in enumerate(sub):
+        assert torch.equal(Ap[j], Af[i])
+
+
+def test_cfg3_full_size_properties(cuda):
+    """BASELINE config 3 at full size (N=2048, T=100, bf16, 4 bags): size-independent checks."""
+    from mcgmil import ops
+    B, N, T, C = 4, 2048, 100, 2
+    arrays = synthetic.head_arrays(synthetic.head_state_dict(0, C=C, shared=False), C, False)
+    head = head_on(arrays, cuda)
+    g = torch.Generator(device=cuda).manual_seed(0)
+    H = torch.randn(B * N, 512, device=cuda, generator=g).abs().bfloat16()
+    offs = ops.bag_offsets_tensor([N] * B, cuda)
+    o1 = ops.mcdo_forward(H, offs, head, T, p_feat=0.1, p_att=0.1, seed=1, return_stats=True)
+    o2 = ops.mcdo_forward(H, offs, head, T, p_feat=0.1, p_att=0.1, seed=1, return_stats=True)
+    for k in o1:
+        assert torch.equal(o1[k], o2[k]), k                      # deterministic
+    A = o1["A"].view(B, T, C, N)
+    assert torch.allclose(A.sum(-1), torch.ones(B, T, C, device=cuda), atol=1e-5)
+    assert bool((A >= 0).all())
+    assert torch.allclose(o1["A_mean"].view(B, C, N).sum(-1), torch.ones(B, C, device=cuda), atol=1e-5)
+    assert torch.allclose(o1["A_mean"].view(B, C, N), A.mean(1), atol=1e-7)
+    assert torch.allclose(o1["A_var"].view(B, C, N), A.var(1), rtol=1e-4, atol=1e-12)
+    p = torch.softmax(o1["Y"], -1).mean(1)
+    assert torch.allclose(o1["P_mean"], p, atol=1e-6)
+    assert o1["Y"].std(1).min() > 0                               # samples differ
+    o0 = ops.mcdo_forward(H, offs, head, T, p_feat=0.0, p_att=0.0, seed=1)
+    assert torch.equal(o0["Y"], o0["Y"][:, :1].expand_as(o0["Y"]))  # p=0: all samples equal
+    o3 = ops.mcdo_forward(H, offs, head, T, p_feat=0.1, p_att=0.1, seed=2)
+    assert not torch.equal(o3["Y"], o1["Y"])                       # seed changes the draw
+
+
+# ------------------------------------------------------------------ drop-in module
+def _flatten_extractor():
+    class Flat(torch.nn.Module):
+        def forward(self, x):
+            return torch.flatten(x, 1)
+    return Flat()
+
+
+def _module(case, cuda):
+    from mcgmil import MultiHeadGatedAttentionMIL
+    _, sd, _ = case.inputs()
+    m = MultiHeadGatedAttentionMIL(num_classes=case.C, pretrained=False, L=case.L, D=case.D,
+                                   feature_dropout=case.p_f, attention_dropout=case.p_a,
+                                   shared_attention=case.shared)
+    own = m.state_dict()
+    missing, unexpected = m.load_state_dict(
+        {k: torch.from_numpy(np.asarray(v)).reshape(own[k].shape) for k, v in sd.items()},
+        strict=False)
+    assert not unexpected and all(k.startswith("feature_extractor") for k in missing)
+    m.feature_extractor = _flatten_extractor()   # feed extracted features as [1, N, L, 1, 1]
+    return m.to(cuda)
+
+
+def test_module_head_keys_match_reference():
+    from mcgmil import MultiHeadGatedAttentionMIL
+    ref = json.load(open(os.path.join(GOLDEN, "reference_head_keys.json")))
+    for shared, tag in ((True, "shared"), (False, "separate")):
+        m = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=shared)
+        own = {k: list(v.shape) for k, v in m.state_dict().items()
+               if not k.startswith("feature_extractor")}
+        assert own == ref[tag]
+
+
+@pytest.mark.parametrize("name", ["cfg2_N512_T30_sep", "cfg2_N512_T30_shared", "small_N64_T1_sep"])
+def test_module_mc_inference_matches_reference(cuda, name):
+    case = Case(name)
+    assert case.bag_ctr == 0
+    m = _module(case, cuda)
+    H, _, _ = case.inputs()
+    x = torch.from_numpy(H).view(1, case.N, case.L, 1, 1)
+    Y, A = m.mc_inference(x, N=case.T, device=cuda, seed=case.mask_seed)
+    assert Y.shape == (case.T, 1, case.C) and A.shape == (case.T, 1, case.C, case.N)
+    np.testing.assert_allclose(Y.cpu().numpy(), case.z["Y"], atol=1e-5)
+    assert nrel(A.cpu().numpy(), case.z["A"]) <= 1e-5
+    Ys, As = m.mc_inference_serial(x, N=case.T, device=cuda, seed=case.mask_seed)
+    assert torch.equal(Ys, Y) and torch.equal(As, A)
+    Y3, A3, losses = m.mc_inference(x, N=case.T, device=cuda, seed=case.mask_seed,
+                                    return_losses=True)
+    assert torch.equal(Y3, Y) and losses is None
+
+
+@pytest.mark.parametrize("name", names("forward"))
+def test_module_forward_eval_matches_reference(cuda, name):
+    case = Case(name)
+    m = _module(case, cuda).eval()
+    H, _, _ = case.inputs()
+    x = torch.from_numpy(H).view(1, case.N, case.L, 1, 1).to(cuda)
+    Y, A, aux = m(x)
+    assert aux is None and Y.shape == (1, case.C) and A.shape == (1, case.C, case.N)
+    np.testing.assert_allclose(Y.cpu().numpy(), case.z["Y"], atol=1e-5)
+    assert nrel(A.cpu().numpy(), case.z["A"]) <= 1e-5
+
+
+def test_module_p0_mc_inference_equals_forward(cuda):
+    case = Case("forward_N64_sep")
+    m = _module(case, cuda)
+    m.feature_dropout.p = 0.0
+    for d in m.attention_dropouts:
+        d.p = 0.0
+    H, _, _ = case.inputs()
+    x = torch.from_numpy(H).view(1, case.N, case.L, 1, 1).to(cuda)
+    Y, A = m.mc_inference(x, N=3, device=cuda, seed=1)
+    Yf, Af, _ = m.eval()(x)
+    for t in range(3):
+        assert torch.equal(Y[t], Yf) and torch.equal(A[t], Af)
+
+
+def test_module_rejects_cpu_and_training(cuda):
+    from mcgmil import MultiHeadGatedAttentionMIL
+    m = MultiHeadGatedAttentionMIL(pretrained=False)
+    with pytest.raises(RuntimeError):
+        m.mc_inference(torch.zeros(1, 2, 3, 32, 32), N=2, device="cpu")
+    m.train()
+    with pytest.raises(NotImplementedError):
+        m(torch.zeros(1, 2, 3, 32, 32))
+
+
+def test_unsupported_config_raises(cuda):
+    from mcgmil import ops, _lib
+    C = 5
+    arrays = synthetic.head_arrays(synthetic.head_state_dict(0, C=C, shared=True), C, True)
+    H = torch.zeros(8, 512, device=cuda)
+    with pytest.raises(_lib.MCGMILError):
+        ops.mcdo_forward(H, ops.bag_offsets_tensor([8], cuda), head_on(arrays, cuda), 2,
+                         p_feat=0.1, p_att=0.1, seed=0)
