@@ -105,30 +105,60 @@ const void* packed_ptr(const mcgmil_args* a) {
     return a->packed_w ? a->packed_w : a->workspace;
 }
 
+template <typename KernelT>
+void raise_lds_cap(KernelT* k) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
 template <typename E, int BM, int PPW, int MAXC>
-int launch_gate(const mcgmil::GateParams& gp, hipStream_t s) {
+int launch_gate_generic(const mcgmil::GateParams& gp, hipStream_t s) {
     auto* k = &mcgmil::gate_scores_kernel<E, BM, PPW, MAXC>;
-    const size_t lds = mcgmil::gate_lds_bytes<E, BM, MAXC>(gp.L);
-    // All scratch is dynamic LDS (> 64 KiB): raise this instantiation's cap once.
-    static std::once_flag once;
-    std::call_once(once, [&] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    });
+    static std::once_flag once;   // per instantiation: all scratch is dynamic LDS (> 64 KiB)
+    std::call_once(once, [&] { raise_lds_cap(k); });
     const long long tiles = (gp.total_samples + BM - 1) / BM;
     if (tiles == 0) return MCGMIL_OK;
+    const size_t lds = mcgmil::gate_lds_bytes<E, BM, MAXC>(gp.L);
     hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(mcgmil::kGateThreads), lds, s, gp);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_scores_kernel launch");
 }
 
-template <typename E, int BM>
-int dispatch_gate_ppw(const mcgmil::GateParams& gp, hipStream_t s) {
-    const bool two = gp.P % (2 * mcgmil::kGateWaves) == 0;
-    if (gp.C <= 2) {
-        return two ? launch_gate<E, BM, 2, 2>(gp, s) : launch_gate<E, BM, 1, 2>(gp, s);
+template <typename E, int PPW, int MAXC, bool REPLAY>
+int launch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
+    auto* k = &mcgmil::gate_pipe_kernel<E, PPW, MAXC, REPLAY>;
+    static std::once_flag once;
+    std::call_once(once, [&] { raise_lds_cap(k); });
+    const long long tiles = (gp.total_samples + mcgmil::kPipeBM - 1) / mcgmil::kPipeBM;
+    if (tiles == 0) return MCGMIL_OK;
+    const size_t lds = mcgmil::pipe_lds_bytes<E, MAXC>();
+    hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(mcgmil::kGateThreads), lds, s, gp);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_pipe_kernel launch");
+}
+
+template <typename E, int MAXC>
+int dispatch_gate_maxc(const mcgmil::GateParams& gp, int L, int dtype, hipStream_t s) {
+    const bool replay = gp.keep_feat != nullptr;
+    const bool pipe_ok = L % 64 == 0;          // the pipelined K loop is unrolled by two steps
+    if (pipe_ok && gp.P <= mcgmil::kGateWaves) {   // one pass, one pair per wave
+        return replay ? launch_gate_pipe<E, 1, MAXC, true>(gp, s)
+                      : launch_gate_pipe<E, 1, MAXC, false>(gp, s);
     }
-    return two ? launch_gate<E, BM, 2, 4>(gp, s) : launch_gate<E, BM, 1, 4>(gp, s);
+    if (pipe_ok && gp.P <= 2 * mcgmil::kGateWaves) {   // one pass, two pairs per wave
+        return replay ? launch_gate_pipe<E, 2, MAXC, true>(gp, s)
+                      : launch_gate_pipe<E, 2, MAXC, false>(gp, s);
+    }
+    // larger heads: whole masked tile in LDS, several passes of 16 pairs
+    return pick_bm(dtype, L) == (dtype == MCGMIL_BF16 ? 128 : 64)
+               ? launch_gate_generic<E, (sizeof(E) == 2 ? 128 : 64), 2, MAXC>(gp, s)
+               : launch_gate_generic<E, (sizeof(E) == 2 ? 32 : 16), 2, MAXC>(gp, s);
+}
+
+template <typename E>
+int dispatch_gate(const mcgmil::GateParams& gp, int L, int dtype, hipStream_t s) {
+    return gp.C <= 2 ? dispatch_gate_maxc<E, 2>(gp, L, dtype, s)
+                     : dispatch_gate_maxc<E, 4>(gp, L, dtype, s);
 }
 
 }  // namespace
@@ -223,10 +253,8 @@ int mcgmil_gate_scores(const mcgmil_args* a, void* stream) {
     gp.zz = reinterpret_cast<float*>(static_cast<char*>(a->workspace) + l.zz_off);
 
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const int bm = pick_bm(a->h_dtype, a->L);
-    if (a->h_dtype == MCGMIL_BF16)
-        return bm == 128 ? dispatch_gate_ppw<__bf16, 128>(gp, s) : dispatch_gate_ppw<__bf16, 32>(gp, s);
-    return bm == 64 ? dispatch_gate_ppw<float, 64>(gp, s) : dispatch_gate_ppw<float, 16>(gp, s);
+    if (a->h_dtype == MCGMIL_BF16) return dispatch_gate<__bf16>(gp, a->L, a->h_dtype, s);
+    return dispatch_gate<float>(gp, a->L, a->h_dtype, s);
 }
 
 int mcgmil_softmax_pool(const mcgmil_args* a, void* stream) {
@@ -251,8 +279,13 @@ int mcgmil_bag_stats(const mcgmil_args* a, void* stream) {
     if ((a->A_mean || a->A_var) && !a->A) return fail(MCGMIL_E_INVALID, "A_mean/A_var need the A output");
     if (!a->Y) return fail(MCGMIL_E_INVALID, "Y is NULL");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(mcgmil::bag_stats_kernel, dim3(a->C, a->num_bags), dim3(256), 0, s,
-                       a->bag_offsets, a->T, a->C, a->A, a->Y, a->A_mean, a->A_var, a->P_mean);
+    const long long outs = (a->A_mean || a->A_var) ? a->total_rows * a->C : 0;
+    const int stat_blocks = (int)((outs + 255) / 256);
+    const int p_blocks = a->P_mean ? (a->num_bags * a->C + 255) / 256 : 0;
+    if (stat_blocks + p_blocks == 0) return MCGMIL_OK;
+    hipLaunchKernelGGL(mcgmil::bag_stats_kernel, dim3(stat_blocks + p_blocks), dim3(256), 0, s,
+                       a->bag_offsets, a->num_bags, a->T, a->C, (long long)a->total_rows,
+                       stat_blocks, a->A, a->Y, a->A_mean, a->A_var, a->P_mean);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "bag_stats_kernel launch");
 }

@@ -43,71 +43,323 @@ struct GateParams {
 
 constexpr int kGateThreads = 512;  // 8 waves
 constexpr int kGateWaves = kGateThreads / kWave;
+constexpr int kRowInfo = 6;        // ints per row: hrow, t, n, bag, Nb, bag counter
 
-constexpr int kRowInfo = 6;  // ints per row: hrow, t, n, bag, Nb, bag counter
+// ---------------------------------------------------------------------------------------
+// Pieces shared by the two gate-score kernels.
+// ---------------------------------------------------------------------------------------
 
+// Row table of one BM-row tile of the flattened (bag, t, n) space (threads < BM).
+template <int BM>
+__device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0, int* rinfo) {
+    const int tid = threadIdx.x;
+    if (tid >= BM) return;
+    const long long R = R0 + tid;
+    int hrow = -1, t = 0, n = 0, bag = 0, Nb = 0;
+    if (R < p.total_samples) {
+        bag = find_bag(p.bag_off, p.B, p.T, R);
+        const int ob = p.bag_off[bag];
+        Nb = p.bag_off[bag + 1] - ob;
+        const long long local = R - (long long)p.T * ob;
+        t = (int)(local / Nb);
+        n = (int)(local - (long long)t * Nb);
+        hrow = ob + n;
+    }
+    int* ri = rinfo + kRowInfo * tid;
+    ri[0] = hrow; ri[1] = t; ri[2] = n; ri[3] = bag; ri[4] = Nb;
+    ri[5] = (int)(p.bag_ids ? p.bag_ids[bag] : p.bag_base + (uint32_t)bag);
+}
+
+// tanh(x) * sigmoid(y) (reference model.py:183-184 / 287) as (1-a) / ((1+a)(1+b)) with
+// a = e^{-2x}, b = e^{-y}: two v_exp_f32 + one v_rcp_f32. x is clamped to +-15, where tanh is
+// already +-1 in fp32, so no inf/inf; b = inf (y < -88) gives the correct 0.
+__device__ __forceinline__ float gated_product(float x, float y) {
+    constexpr float kM2Log2e = -2.8853900817779268f;   // -2 / ln 2
+    constexpr float kMLog2e = -1.4426950408889634f;    // -1 / ln 2
+    x = fminf(fmaxf(x, -15.0f), 15.0f);
+    const float a = __builtin_amdgcn_exp2f(x * kM2Log2e);
+    const float b = __builtin_amdgcn_exp2f(y * kMLog2e);
+    return (1.0f - a) * __builtin_amdgcn_rcpf((1.0f + a) * (1.0f + b));
+}
+
+// Fold the gate pairs of one pass into per-lane partial scores. acc[rt][2j] / acc[rt][2j+1]
+// hold V / U pre-activations of pair q0 + j for instance rt*16 + (lane & 15) and
+// d = 16*db + 4*(lane >> 4) + v (16x16 C layout with the weights as the A operand).
+template <int RT, int PPW, int MAXC>
+__device__ __forceinline__ void fold_pairs(const GateParams& p, const f32x4 (&acc)[RT][2 * PPW],
+                                           int q0, int lane, float (&part)[MAXC][RT]) {
+    const int DB = p.D >> 4;
+#pragma unroll
+    for (int jp = 0; jp < PPW; ++jp) {
+        const int q = q0 + jp;
+        if (q >= p.P) break;
+        const int g = q / DB, db = q - g * DB;
+        const int d0 = db * 16 + 4 * (lane >> 4);
+        const f32x4 bvv = *reinterpret_cast<const f32x4*>(p.bv + (size_t)g * p.D + d0);
+        const f32x4 buv = *reinterpret_cast<const f32x4*>(p.bu + (size_t)g * p.D + d0);
+        f32x4 coef[MAXC];
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            const bool use = (c < p.C) && (p.G == 1 || c == g);
+            // address stays inside wa[C, D] for every c; unused classes get 0
+            const f32x4 w = *reinterpret_cast<const f32x4*>(p.wa + (size_t)(use ? c : 0) * p.D + d0);
+            coef[c] = use ? w : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const float pr = gated_product(fmaf(acc[rt][2 * jp][v], p.sf, bvv[v]),
+                                               fmaf(acc[rt][2 * jp + 1][v], p.sf, buv[v]));
+#pragma unroll
+                for (int c = 0; c < MAXC; ++c) part[c][rt] = fmaf(pr, coef[c][v], part[c][rt]);
+            }
+        }
+    }
+}
+
+// Cross-wave reduction of the partial scores + attention bias, logit dropout and stores
+// (model.py:289-291 / 299-301); z = sf * (X . k_c) for the classifier (model.py:313-315).
+template <int BM, int MAXC>
+__device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
+                                              float (&part)[MAXC][BM / 16], f32x4 zacc,
+                                              bool zwave, float* red, float* zred,
+                                              const int* rinfo) {
+    constexpr int RT = BM / 16;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            float v = part[c][rt];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            if (lane < 16) red[(wave * MAXC + c) * BM + rt * 16 + lane] = v;
+        }
+    if (zwave && lane < 16) {
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) zred[c * BM + wave * 16 + lane] = zacc[c];
+    }
+    __syncthreads();
+    for (int i = tid; i < BM * p.C; i += kGateThreads) {
+        const int c = i / BM, r = i - c * BM;
+        const int* ri = rinfo + kRowInfo * r;
+        if (ri[0] < 0) continue;
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < kGateWaves; ++w) s += red[(w * MAXC + c) * BM + r];
+        s += p.ba[c];
+        const int t = ri[1], n = ri[2], bag = ri[3], Nb = ri[4];
+        bool keep;
+        if (p.keep_att) {
+            const size_t abase = (size_t)p.T * p.C * (size_t)p.bag_off[bag];
+            keep = p.keep_att[abase + ((size_t)t * p.C + c) * Nb + n] != 0;
+        } else {
+            keep = attention_keep(p.k0, p.k1, (uint32_t)ri[5], (uint32_t)(p.t_base + t),
+                                  (uint32_t)c, (uint32_t)n, p.thr_a);
+        }
+        const size_t o = (size_t)(R0 + r) * p.C + c;
+        p.logits[o] = s * (keep ? p.sa : 0.f);
+        p.zz[o] = zred[c * BM + r] * p.sf;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// gate_pipe_kernel -- the fast path (gate tile pairs P <= 16, i.e. one pass: the reference's
+// C=2/D=128 heads, shared or separate). One workgroup = 128 rows of the flattened (bag, t, n)
+// space, 8 waves. The masked features are never materialised whole: the K loop runs over
+// 32-deep steps and, while the MFMAs consume step s from one LDS slot, every thread draws
+// ONE Philox4x32-10 block (8 keep decisions = its 8-element fragment chunk) for step s+1,
+// masks the H chunk it loaded one step earlier and writes it into the other slot (one
+// barrier per step). Wave w owns gate tile pairs w*PPW .. w*PPW+PPW-1 for all 128 rows,
+// weight fragments streamed from L2 one step ahead, plus the classifier tile for row tile w.
+// ---------------------------------------------------------------------------------------
+template <typename E> struct Raw;
+template <> struct Raw<__bf16> { uint4 v; };
+template <> struct Raw<float> { f32x4 lo, hi; };
+__device__ __forceinline__ Raw<__bf16> load_raw(const __bf16* p) {
+    Raw<__bf16> r; r.v = *reinterpret_cast<const uint4*>(p); return r;
+}
+__device__ __forceinline__ Raw<float> load_raw(const float* p) {
+    Raw<float> r;
+    r.lo = *reinterpret_cast<const f32x4*>(p);
+    r.hi = *reinterpret_cast<const f32x4*>(p + 4);
+    return r;
+}
+__device__ __forceinline__ void store_masked(const Raw<__bf16>& h, uint32_t kb, __bf16* dst) {
+    uint4 v = h.v;
+    v.x &= ((kb & 1u) ? 0x0000FFFFu : 0u) | ((kb & 2u) ? 0xFFFF0000u : 0u);
+    v.y &= ((kb & 4u) ? 0x0000FFFFu : 0u) | ((kb & 8u) ? 0xFFFF0000u : 0u);
+    v.z &= ((kb & 16u) ? 0x0000FFFFu : 0u) | ((kb & 32u) ? 0xFFFF0000u : 0u);
+    v.w &= ((kb & 64u) ? 0x0000FFFFu : 0u) | ((kb & 128u) ? 0xFFFF0000u : 0u);
+    *reinterpret_cast<uint4*>(dst) = v;
+}
+__device__ __forceinline__ void store_masked(const Raw<float>& h, uint32_t kb, float* dst) {
+    f32x4 a = h.lo, b = h.hi;
+    a.x = (kb & 1u) ? a.x : 0.f;   a.y = (kb & 2u) ? a.y : 0.f;
+    a.z = (kb & 4u) ? a.z : 0.f;   a.w = (kb & 8u) ? a.w : 0.f;
+    b.x = (kb & 16u) ? b.x : 0.f;  b.y = (kb & 32u) ? b.y : 0.f;
+    b.z = (kb & 64u) ? b.z : 0.f;  b.w = (kb & 128u) ? b.w : 0.f;
+    *reinterpret_cast<f32x4*>(dst) = a;
+    *reinterpret_cast<f32x4*>(dst + 4) = b;
+}
+
+constexpr int kPipeBM = 128;
+
+template <typename E, int MAXC>
+__host__ __device__ constexpr size_t pipe_lds_bytes() {
+    return (size_t)2 * kPipeBM * 32 * sizeof(E) + (size_t)kGateWaves * MAXC * kPipeBM * 4 +
+           (size_t)MAXC * kPipeBM * 4 + (size_t)kRowInfo * kPipeBM * 4;
+}
+
+template <typename E, int PPW, int MAXC, bool REPLAY>
+__global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int BM = kPipeBM;
+    constexpr int RT = BM / 16;                     // 8 row tiles = 8 waves
+    constexpr int NJ = 2 * PPW;
+    constexpr int SLOT = RT * 64 * 8;               // elements of one 32-deep K step
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int KS = p.L >> 5;
+
+    E* Xs = reinterpret_cast<E*>(smem);                                   // [2][SLOT]
+    float* red = reinterpret_cast<float*>(smem + (size_t)2 * SLOT * sizeof(E));
+    float* zred = red + kGateWaves * MAXC * BM;
+    int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);
+    const long long R0 = (long long)blockIdx.x * BM;
+
+    fill_row_table<BM>(p, R0, rinfo);
+    __syncthreads();
+
+    // staging item of this thread: row wave*16 + (lane & 15), 8-chunk kq = lane >> 4 of
+    // every K step; it lands at lane slot `lane` of row tile `wave` (= element tid*8)
+    const int* ri = rinfo + kRowInfo * (wave * 16 + (lane & 15));
+    const int hrow = ri[0];
+    const bool valid = hrow >= 0;
+    const int kq = lane >> 4;
+    const E* hsrc = reinterpret_cast<const E*>(p.H) + (size_t)(valid ? hrow : 0) * p.ldh + kq * 8;
+    const uint32_t cn = (uint32_t)ri[2], ct = (uint32_t)(p.t_base + ri[1]), cb = (uint32_t)ri[5];
+    // replay row (row 0 for padding rows, whose bits are masked off by vmask)
+    const uint8_t* kfe = REPLAY ? p.keep_feat + (size_t)(valid ? R0 + wave * 16 + (lane & 15) : 0) *
+                                                    (p.L >> 3) + kq
+                                : nullptr;
+    const uint32_t vmask = valid ? 0xFFu : 0u;
+
+    auto stage = [&](int s, const Raw<E>& h, E* slot) {
+        uint32_t kb;
+        if constexpr (REPLAY) {
+            kb = kfe[(size_t)(s < KS ? s : KS - 1) * 4];   // step KS is a dummy: stay in the row
+        } else {
+            kb = keep_byte(philox4x32_10((uint32_t)(s * 4 + kq), cn, ct, cb, p.k0, p.k1), p.thr_f);
+        }
+        store_masked(h, kb & vmask, slot + tid * 8);
+    };
+
+    // weight tiles of this wave (idle pair slots read a valid tile; fold_pairs skips them)
+    const E* Wp = reinterpret_cast<const E*>(p.Wp);
+    const size_t tile_elems = (size_t)KS * 512;
+    const int q0 = wave * PPW;
+    const E* wbase[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        int q = q0 + (j >> 1);
+        q = q < p.P ? q : p.P - 1;
+        wbase[j] = Wp + (size_t)(2 * q + (j & 1)) * tile_elems + lane * 8;
+    }
+    const E* zbase = Wp + (size_t)(2 * p.P) * tile_elems + lane * 8;
+
+    f32x4 acc[RT][NJ];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 zacc = {0.f, 0.f, 0.f, 0.f};
+
+    // One K step: MFMAs on step s from slot `cur` with weights (w, z); meanwhile prefetch the
+    // weights of step s+1 into (wn, zn) and the H chunk of step s+2 into hn, and stage step
+    // s+1 (from h, loaded one step earlier) into slot `nxt`. Loop-carried values alternate
+    // between two NAMED register sets (the loop is unrolled by two), so no register copy
+    // forces an early wait on the prefetches.
+    auto kstep = [&](int s, const E* cur, E* nxt, const Frag<E> (&w)[NJ], const Frag<E>& z,
+                     Frag<E> (&wn)[NJ], Frag<E>& zn, const Raw<E>& h, Raw<E>& hn) {
+        const int s1 = s + 1 < KS ? s + 1 : KS - 1;          // clamped: no branch in the body
+        const int s2 = s + 2 < KS ? s + 2 : KS - 1;
+        hn = load_raw(hsrc + (size_t)s2 * 32);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) wn[j] = load_frag(wbase[j] + (size_t)s1 * 512);
+        zn = load_frag(zbase + (size_t)s1 * 512);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const Frag<E> x = load_frag(cur + (size_t)(rt * 64 + lane) * 8);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[rt][j] = mma(w[j], x, acc[rt][j]);
+        }
+        const Frag<E> xz = load_frag(cur + (size_t)tid * 8);  // row tile `wave`
+        zacc = mma(z, xz, zacc);
+        stage(s + 1, h, nxt);           // step KS is staged into the idle slot and never read
+        __syncthreads();
+    };
+
+    // prologue: stage step 0, load H of step 1 and the weights of step 0
+    Frag<E> wA[NJ], wB[NJ], zA, zB;
+    Raw<E> hA, hB;
+    hA = load_raw(hsrc);
+    stage(0, hA, Xs);
+    hB = load_raw(hsrc + 32);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) wA[j] = load_frag(wbase[j]);
+    zA = load_frag(zbase);
+    __syncthreads();
+
+    for (int s = 0; s < KS; s += 2) {     // KS is even (host guarantees L % 64 == 0)
+        kstep(s, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA);
+        kstep(s + 1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB);
+    }
+
+    float part[MAXC][RT];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) part[c][rt] = 0.f;
+    fold_pairs<RT, PPW, MAXC>(p, acc, q0, lane, part);
+    finish_scores<BM, MAXC>(p, R0, part, zacc, true, red, zred, rinfo);
+}
+
+// ---------------------------------------------------------------------------------------
+// gate_scores_kernel -- the generic path (any P): the whole masked BM x L feature tile is
+// staged in LDS once, then the gate tile pairs are computed in passes of 8*PPW pairs.
+// ---------------------------------------------------------------------------------------
 template <int BM>
 __host__ __device__ constexpr int gate_row_info_ints() { return kRowInfo * BM; }
 
-// Dynamic LDS of gate_scores_kernel: [X tile BM*L elems][red NW*MAXC*BM f32][zred MAXC*BM f32]
-// [row info 5*BM i32]. Every carve offset is a multiple of 16 bytes.
 template <typename E, int BM, int MAXC>
 __host__ __device__ constexpr size_t gate_lds_bytes(int L) {
     return (size_t)BM * L * sizeof(E) + (size_t)kGateWaves * MAXC * BM * 4 + (size_t)MAXC * BM * 4 +
            (size_t)gate_row_info_ints<BM>() * 4;
 }
 
-// ---------------------------------------------------------------------------------------
-// gate_scores_kernel: one workgroup = BM rows of the flattened (bag, t, n) space.
-//   phase 1: row table (bag, t, n) in LDS;
-//   phase 2: stage X = H (.) keep for the BM rows into LDS as MFMA B fragments
-//            (one Philox4x32-10 block = 8 keep decisions = one 8-element fragment chunk);
-//   phase 3: per pass, wave w computes gate tile pairs (V_q, U_q) for all BM rows with the
-//            weight fragments streamed from L2 (packed, one 16-B load per lane), and folds
-//            tanh*sigmoid*wa into per-lane partial scores; waves w < BM/16 also compute the
-//            classifier projection z for row tile w;
-//   phase 4: cross-wave reduction, bias, attention dropout, store s' and z.
-// ---------------------------------------------------------------------------------------
 template <typename E, int BM, int PPW, int MAXC>
 __global__ __launch_bounds__(kGateThreads) void gate_scores_kernel(const GateParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int RT = BM / 16;        // 16-row tiles per workgroup
-    constexpr int NJ = 2 * PPW;        // weight column tiles per wave per pass
+    constexpr int RT = BM / 16;
+    constexpr int NJ = 2 * PPW;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int L = p.L;
-    const int KS = L >> 5;             // 32-deep K steps
-    const int LC = L >> 3;             // 8-element chunks per row
+    const int KS = L >> 5;
+    const int LC = L >> 3;
 
     E* Xs = reinterpret_cast<E*>(smem);
     float* red = reinterpret_cast<float*>(smem + (size_t)BM * L * sizeof(E));
     float* zred = red + kGateWaves * MAXC * BM;
-    int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);  // [r][kRowInfo]
-
+    int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);
     const long long R0 = (long long)blockIdx.x * BM;
 
-    // ---- phase 1: row table ----
-    if (tid < BM) {
-        const long long R = R0 + tid;
-        int hrow = -1, t = 0, n = 0, bag = 0, Nb = 0;
-        if (R < p.total_samples) {
-            bag = find_bag(p.bag_off, p.B, p.T, R);
-            const int ob = p.bag_off[bag];
-            Nb = p.bag_off[bag + 1] - ob;
-            const long long local = R - (long long)p.T * ob;
-            t = (int)(local / Nb);
-            n = (int)(local - (long long)t * Nb);
-            hrow = ob + n;
-        }
-        int* ri = rinfo + kRowInfo * tid;
-        ri[0] = hrow; ri[1] = t; ri[2] = n; ri[3] = bag; ri[4] = Nb;
-        ri[5] = (int)(p.bag_ids ? p.bag_ids[bag] : p.bag_base + (uint32_t)bag);
-    }
+    fill_row_table<BM>(p, R0, rinfo);
     __syncthreads();
 
-    // ---- phase 2: stage the masked feature tile ----
-    {
+    {   // stage the masked feature tile
         const E* H = reinterpret_cast<const E*>(p.H);
         const int items = BM * LC;
         for (int i = tid; i < items; i += kGateThreads) {
@@ -136,13 +388,10 @@ __global__ __launch_bounds__(kGateThreads) void gate_scores_kernel(const GatePar
     }
     __syncthreads();
 
-    // ---- phase 3: gate GEMM + fused epilogue ----
     const E* Wp = reinterpret_cast<const E*>(p.Wp);
-    const int DB = p.D >> 4;                   // 16-wide d blocks per gate
     const int pairs_per_pass = kGateWaves * PPW;
     const int npass = (p.P + pairs_per_pass - 1) / pairs_per_pass;
-    const size_t tile_elems = (size_t)KS * 512;  // one packed 16-column tile
-    const int lgrp = lane >> 4;                 // 4-row group inside the 16x16 accumulator
+    const size_t tile_elems = (size_t)KS * 512;
 
     float part[MAXC][RT];
 #pragma unroll
@@ -168,7 +417,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_scores_kernel(const GatePar
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             int q = q0 + (j >> 1);
-            q = q < p.P ? q : p.P - 1;             // idle slots read a valid tile, unused
+            q = q < p.P ? q : p.P - 1;
             wbase[j] = Wp + (size_t)(2 * q + (j & 1)) * tile_elems + lane * 8;
         }
         const E* zbase = Wp + (size_t)(2 * p.P) * tile_elems + lane * 8;
@@ -199,76 +448,10 @@ __global__ __launch_bounds__(kGateThreads) void gate_scores_kernel(const GatePar
             for (int j = 0; j < NJ; ++j) wcur[j] = wnxt[j];
             zcur = znxt;
         }
-
         if (!active) continue;
-        // epilogue: lane holds instance rt*16 + (lane & 15), d = db*16 + 4*lgrp + v
-#pragma unroll
-        for (int jp = 0; jp < PPW; ++jp) {
-            const int q = q0 + jp;
-            if (q >= p.P) break;
-            const int g = q / DB, db = q - g * DB;
-            const int d0 = db * 16 + 4 * lgrp;
-            const f32x4 bvv = *reinterpret_cast<const f32x4*>(p.bv + (size_t)g * p.D + d0);
-            const f32x4 buv = *reinterpret_cast<const f32x4*>(p.bu + (size_t)g * p.D + d0);
-            f32x4 coef[MAXC];
-#pragma unroll
-            for (int c = 0; c < MAXC; ++c) {
-                const bool use = (c < p.C) && (p.G == 1 || c == g);
-                // address stays inside wa[C, D] for every c; unused classes get 0
-                const f32x4 w = *reinterpret_cast<const f32x4*>(p.wa + (size_t)(use ? c : 0) * p.D + d0);
-                coef[c] = use ? w : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt) {
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const float av = gate_tanh(acc[rt][2 * jp][v] * p.sf + bvv[v]);
-                    const float au = gate_sigmoid(acc[rt][2 * jp + 1][v] * p.sf + buv[v]);
-                    const float pr = av * au;
-#pragma unroll
-                    for (int c = 0; c < MAXC; ++c) part[c][rt] = fmaf(pr, coef[c][v], part[c][rt]);
-                }
-            }
-        }
+        fold_pairs<RT, PPW, MAXC>(p, acc, q0, lane, part);
     }
-
-    // ---- phase 4: reductions, bias, attention dropout, stores ----
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-            float v = part[c][rt];
-            v += __shfl_xor(v, 16);
-            v += __shfl_xor(v, 32);
-            if (lane < 16) red[(wave * MAXC + c) * BM + rt * 16 + lane] = v;
-        }
-    if (zwave && lane < 16) {
-#pragma unroll
-        for (int c = 0; c < MAXC; ++c) zred[c * BM + wave * 16 + lane] = zacc[c];
-    }
-    __syncthreads();
-
-    for (int i = tid; i < BM * p.C; i += kGateThreads) {
-        const int c = i / BM, r = i - c * BM;
-        const int* ri = rinfo + kRowInfo * r;
-        if (ri[0] < 0) continue;
-        float s = 0.f;
-#pragma unroll
-        for (int w = 0; w < kGateWaves; ++w) s += red[(w * MAXC + c) * BM + r];
-        s += p.ba[c];
-        const int t = ri[1], n = ri[2], bag = ri[3], Nb = ri[4];
-        bool keep;
-        if (p.keep_att) {
-            const size_t abase = (size_t)p.T * p.C * (size_t)p.bag_off[bag];
-            keep = p.keep_att[abase + ((size_t)t * p.C + c) * Nb + n] != 0;
-        } else {
-            keep = attention_keep(p.k0, p.k1, (uint32_t)ri[5], (uint32_t)(p.t_base + t),
-                                  (uint32_t)c, (uint32_t)n, p.thr_a);
-        }
-        const size_t o = (size_t)(R0 + r) * p.C + c;
-        p.logits[o] = s * (keep ? p.sa : 0.f);
-        p.zz[o] = zred[c * BM + r] * p.sf;
-    }
+    finish_scores<BM, MAXC>(p, R0, part, zacc, zwave, red, zred, rinfo);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -322,49 +505,50 @@ __global__ __launch_bounds__(256) void softmax_pool_kernel(const int32_t* bag_of
 }
 
 // ---------------------------------------------------------------------------------------
-// bag_stats_kernel: one 256-thread block per (class, bag). Mean and unbiased variance of the
-// attention over the T passes (infer.py:216-219: torch .mean/.std, var = std^2) and the mean
-// class probability (infer.py:195 softmax over classes; net_utils.py:207-208 mean over T).
+// bag_stats_kernel: mean and unbiased variance of the attention over the T passes
+// (infer.py:216-219: torch .mean/.std, var = std^2) -- one thread per output (bag, c, n),
+// coalesced over n -- and, in the trailing blocks, the mean class probability per (bag, c)
+// (infer.py:195 softmax over classes; net_utils.py:207-208 mean over T). Sums in fp64.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void bag_stats_kernel(const int32_t* bag_off, int T, int C,
+__global__ __launch_bounds__(256) void bag_stats_kernel(const int32_t* bag_off, int B, int T, int C,
+                                                        long long total_rows, int stat_blocks,
                                                         const float* A, const float* Y,
                                                         float* A_mean, float* A_var, float* P_mean) {
-    __shared__ double sred[4];
-    const int c = blockIdx.x, b = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int ob = bag_off[b];
-    const int Nb = bag_off[b + 1] - ob;
-    if (A && (A_mean || A_var)) {
-        const size_t abase = (size_t)T * C * ob + (size_t)c * Nb;
-        const size_t sbase = (size_t)C * ob + (size_t)c * Nb;
-        for (int n = tid; n < Nb; n += 256) {
-            double s = 0.0;
-            for (int t = 0; t < T; ++t) s += A[abase + (size_t)t * C * Nb + n];
-            const double mean = s / T;
-            double ss = 0.0;
-            for (int t = 0; t < T; ++t) {
-                const double d = (double)A[abase + (size_t)t * C * Nb + n] - mean;
-                ss += d * d;
-            }
-            if (A_mean) A_mean[sbase + n] = (float)mean;
-            if (A_var) A_var[sbase + n] = T > 1 ? (float)(ss / (T - 1)) : NAN;
+    if ((int)blockIdx.x < stat_blocks) {
+        const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+        if (i >= total_rows * C) return;
+        const int bag = find_bag(bag_off, B, C, i);
+        const int ob = bag_off[bag];
+        const int Nb = bag_off[bag + 1] - ob;
+        const long long local = i - (long long)C * ob;
+        const int c = (int)(local / Nb);
+        const int n = (int)(local - (long long)c * Nb);
+        const float* a = A + (size_t)T * C * ob + (size_t)c * Nb + n;
+        const size_t step = (size_t)C * Nb;
+        double s = 0.0, ss = 0.0;
+        for (int t = 0; t < T; ++t) {
+            const double v = a[(size_t)t * step];
+            s += v;
+            ss += v * v;
         }
+        const double mean = s / T;
+        if (A_mean) A_mean[i] = (float)mean;
+        if (A_var) A_var[i] = T > 1 ? (float)fmax((ss - s * mean) / (T - 1), 0.0) : NAN;
+        return;
     }
-    if (P_mean) {
-        double acc = 0.0;
-        for (int t = tid; t < T; t += 256) {
-            const float* y = Y + ((size_t)b * T + t) * C;
-            float m = y[0];
-            for (int k = 1; k < C; ++k) m = fmaxf(m, y[k]);
-            float s = 0.f;
-            for (int k = 0; k < C; ++k) s += expf(y[k] - m);
-            acc += (double)(expf(y[c] - m) / s);
-        }
-        acc = wave_sum_d(acc);
-        if (lane == 0) sred[wave] = acc;
-        __syncthreads();
-        if (tid == 0) P_mean[(size_t)b * C + c] = (float)(((sred[0] + sred[1]) + (sred[2] + sred[3])) / T);
+    const int j = ((int)blockIdx.x - stat_blocks) * 256 + threadIdx.x;
+    if (!P_mean || j >= B * C) return;
+    const int b = j / C, c = j - b * C;
+    double acc = 0.0;
+    for (int t = 0; t < T; ++t) {
+        const float* y = Y + ((size_t)b * T + t) * C;
+        float m = y[0];
+        for (int k = 1; k < C; ++k) m = fmaxf(m, y[k]);
+        float sum = 0.f;
+        for (int k = 0; k < C; ++k) sum += expf(y[k] - m);
+        acc += (double)(expf(y[c] - m) / sum);
     }
+    P_mean[j] = (float)(acc / T);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -31,6 +31,7 @@ for s in $STEPS; do
         smoke) run smoke 420 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
         tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
         bench) run bench 600 python bench.py ;;
+        probe) run probe 300 python scripts/probe_gate.py ;;
         prof)
             rm -rf "$OUT/prof_$TAG"
             run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run \

@@ -64,12 +64,16 @@ def compare(case, out, tol):
         assert nrel(A[0], case.z["A_first"][0]) <= tol["A"]
         assert nrel(A[-1], case.z["A_last"][0]) <= tol["A"]
     Am = out["A_mean"].reshape(C, N)
-    assert nrel(Am, case.z["A_mean"][0]) <= tol["A_mean"]
-    assert np.max(np.abs(Am - case.z["A_mean"][0])) <= 1e-4        # the north-star bound
+    assert case.z["A_mean"].shape == (C, N)
+    assert nrel(Am, case.z["A_mean"]) <= tol["A_mean"]
+    assert np.max(np.abs(Am - case.z["A_mean"])) <= 1e-4            # the north-star bound
     Av = out["A_var"].reshape(C, N)
     if T > 1:
-        assert nrel(Av, case.z["A_var"][0]) <= tol["A_var"]
-        assert np.max(np.abs(Av - case.z["A_var"][0])) <= 1e-4
+        # nrel, or an absolute floor far below any real variance (A ~ 1/N, var ~ 1e-8): the
+        # reference's own fp32 var of T identical values is rounding noise (~1e-20), ours 0
+        dv = np.max(np.abs(Av - case.z["A_var"]))
+        assert nrel(Av, case.z["A_var"]) <= tol["A_var"] or dv <= 1e-15
+        assert dv <= 1e-4
     else:
         assert np.isnan(Av).all()
     np.testing.assert_allclose(out["P_mean"][0], case.z["P_mean"], rtol=0, atol=tol["P_mean"])
@@ -87,7 +91,7 @@ def test_masks_bit_exact(cuda):
     ka = ops.attention_keep(offs, R, T, C, 0.3, seed, bag_id_base=base, t_base=3).cpu().numpy()
     rf = ra = 0
     for b, n in enumerate(sizes):
-        want_f = philox.feature_keep_bits(seed, base + b, T, n, L, 0.1, t0=3).reshape(T * n, -1)
+        want_f = philox.feature_keep_bits(seed, base + b, T, n, L, 0.1, t0=3).reshape(T * n, L // 8)
         want_a = philox.attention_keep(seed, base + b, T, C, n, 0.3, t0=3).astype(np.uint8).reshape(-1)
         assert np.array_equal(kf[rf:rf + T * n], want_f), b
         assert np.array_equal(ka[ra:ra + T * C * n], want_a), b
