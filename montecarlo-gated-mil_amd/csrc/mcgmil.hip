@@ -124,9 +124,9 @@ int launch_gate_generic(const mcgmil::GateParams& gp, hipStream_t s) {
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_scores_kernel launch");
 }
 
-template <typename E, int PPW, int MAXC, bool REPLAY>
+template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE>
 int launch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
-    auto* k = &mcgmil::gate_pipe_kernel<E, PPW, MAXC, REPLAY>;
+    auto* k = &mcgmil::gate_pipe_kernel<E, PPW, MAXC, REPLAY, ONE>;
     static std::once_flag once;
     std::call_once(once, [&] { raise_lds_cap(k); });
     const long long tiles = (gp.total_samples + mcgmil::kPipeBM - 1) / mcgmil::kPipeBM;
@@ -137,18 +137,22 @@ int launch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_pipe_kernel launch");
 }
 
+template <typename E, int PPW, int MAXC>
+int dispatch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
+    const bool replay = gp.keep_feat != nullptr;
+    // separate heads whose gate tile pairs split evenly over the waves: one class per wave
+    const bool one = gp.G > 1 && gp.G == gp.C && (gp.D / 16) % PPW == 0;
+    if (replay) return one ? launch_gate_pipe<E, PPW, MAXC, true, true>(gp, s)
+                           : launch_gate_pipe<E, PPW, MAXC, true, false>(gp, s);
+    return one ? launch_gate_pipe<E, PPW, MAXC, false, true>(gp, s)
+               : launch_gate_pipe<E, PPW, MAXC, false, false>(gp, s);
+}
+
 template <typename E, int MAXC>
 int dispatch_gate_maxc(const mcgmil::GateParams& gp, int L, int dtype, hipStream_t s) {
-    const bool replay = gp.keep_feat != nullptr;
     const bool pipe_ok = L % 64 == 0;          // the pipelined K loop is unrolled by two steps
-    if (pipe_ok && gp.P <= mcgmil::kGateWaves) {   // one pass, one pair per wave
-        return replay ? launch_gate_pipe<E, 1, MAXC, true>(gp, s)
-                      : launch_gate_pipe<E, 1, MAXC, false>(gp, s);
-    }
-    if (pipe_ok && gp.P <= 2 * mcgmil::kGateWaves) {   // one pass, two pairs per wave
-        return replay ? launch_gate_pipe<E, 2, MAXC, true>(gp, s)
-                      : launch_gate_pipe<E, 2, MAXC, false>(gp, s);
-    }
+    if (pipe_ok && gp.P <= mcgmil::kGateWaves) return dispatch_gate_pipe<E, 1, MAXC>(gp, s);
+    if (pipe_ok && gp.P <= 2 * mcgmil::kGateWaves) return dispatch_gate_pipe<E, 2, MAXC>(gp, s);
     // larger heads: whole masked tile in LDS, several passes of 16 pairs
     return pick_bm(dtype, L) == (dtype == MCGMIL_BF16 ? 128 : 64)
                ? launch_gate_generic<E, (sizeof(E) == 2 ? 128 : 64), 2, MAXC>(gp, s)
@@ -242,6 +246,7 @@ int mcgmil_gate_scores(const mcgmil_args* a, void* stream) {
     gp.sa = dropout_scale(a->p_att);
     gp.thr_f = drop_threshold(a->p_feat);
     gp.thr_a = drop_threshold(a->p_att);
+    gp.thrx_f = mcgmil::packed_threshold(gp.thr_f);
     gp.k0 = (uint32_t)a->seed;
     gp.k1 = (uint32_t)(a->seed >> 32);
     gp.bag_base = a->bag_id_base;

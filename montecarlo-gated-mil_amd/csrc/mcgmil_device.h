@@ -18,17 +18,34 @@ __device__ __forceinline__ uint4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_
                                                uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t lo0 = 0xD2511F53u * c0;
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
-        const uint32_t n0 = hi1 ^ c1 ^ k0;
-        const uint32_t n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        // one v_mad_u64_u32 per product gives both halves (measured: the cost of one
+        // v_mul_hi_u32, half of a separate mul_lo + mul_hi pair)
+        const uint64_t p0 = (uint64_t)c0 * 0xD2511F53u;
+        const uint64_t p1 = (uint64_t)c2 * 0xCD9E8D57u;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
     return make_uint4(c0, c1, c2, c3);
+}
+
+// Packed form of the keep rule for the two 16-bit draws of one Philox word: returns 0xFFFF in
+// each half whose draw is DROPPED (u16 < thr) and 0 where it is kept. thrx = the threshold
+// (clamped to 65535; p = 1 is handled by the zero dropout scale) with its sign bit flipped, in
+// both halves: u >= thr (unsigned) <=> (u ^ 0x8000) >= (thr ^ 0x8000) (signed), and a
+// saturating signed difference keeps the sign. v_xor + v_pk_sub_i16 clamp + v_pk_ashrrev_i16.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t drop_mask16x2(uint32_t word, uint32_t thrx) {
+    const s16x2 u = __builtin_bit_cast(s16x2, word ^ 0x80008000u);
+    const s16x2 d = __builtin_elementwise_sub_sat(u, __builtin_bit_cast(s16x2, thrx));
+    return __builtin_bit_cast(uint32_t, d >> (s16x2){15, 15});
+}
+
+__host__ __device__ inline uint32_t packed_threshold(uint32_t thr) {
+    const uint32_t t = (thr > 65535u ? 65535u : thr) ^ 0x8000u;
+    return t | (t << 16);
 }
 
 // Eight keep decisions (bit m = draw m) from one Philox block: keep iff u16 >= thr.
@@ -127,16 +144,6 @@ __device__ __forceinline__ void store_zero8(__bf16* dst) {
 __device__ __forceinline__ void store_zero8(float* dst) {
     *reinterpret_cast<f32x4*>(dst) = f32x4{0.f, 0.f, 0.f, 0.f};
     *reinterpret_cast<f32x4*>(dst + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
-}
-
-// Gate nonlinearities (reference model.py:183-184: nn.Tanh / nn.Sigmoid), via v_exp_f32 and
-// v_rcp_f32. Saturate correctly at +-inf arguments.
-__device__ __forceinline__ float gate_tanh(float x) {
-    const float e = __expf(2.0f * x);
-    return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
-}
-__device__ __forceinline__ float gate_sigmoid(float x) {
-    return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
 }
 
 // Bag lookup in the flattened (bag, t, n) row space: largest b with T*off[b] <= R.

@@ -31,6 +31,7 @@ struct GateParams {
     const float* ba;
     float sf, sa;                  // dropout scales 1/(1-p) (0 for p = 1)
     uint32_t thr_f, thr_a;         // 16-bit drop thresholds
+    uint32_t thrx_f;               // packed_threshold(thr_f)
     uint32_t k0, k1;               // Philox key = seed
     uint32_t bag_base;
     int t_base;
@@ -70,49 +71,63 @@ __device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0
     ri[5] = (int)(p.bag_ids ? p.bag_ids[bag] : p.bag_base + (uint32_t)bag);
 }
 
-// tanh(x) * sigmoid(y) (reference model.py:183-184 / 287) as (1-a) / ((1+a)(1+b)) with
-// a = e^{-2x}, b = e^{-y}: two v_exp_f32 + one v_rcp_f32. x is clamped to +-15, where tanh is
-// already +-1 in fp32, so no inf/inf; b = inf (y < -88) gives the correct 0.
-__device__ __forceinline__ float gated_product(float x, float y) {
-    constexpr float kM2Log2e = -2.8853900817779268f;   // -2 / ln 2
-    constexpr float kMLog2e = -1.4426950408889634f;    // -1 / ln 2
-    x = fminf(fmaxf(x, -15.0f), 15.0f);
-    const float a = __builtin_amdgcn_exp2f(x * kM2Log2e);
-    const float b = __builtin_amdgcn_exp2f(y * kMLog2e);
-    return (1.0f - a) * __builtin_amdgcn_rcpf((1.0f + a) * (1.0f + b));
+// tanh(x) * sigmoid(y) (reference model.py:183-184 / 287) evaluated as (1-a) / ((1+a)(1+b)),
+// a = e^{-2x} = 2^{ax}, b = e^{-y} = 2^{by}, from the pre-scaled arguments
+// ax = -2 log2(e) x, by = -log2(e) y (the scaling is folded into the GEMM epilogue FMA):
+// two v_exp_f32 + one v_rcp_f32. ax is clamped to +-15 * 2 log2(e), where tanh is already +-1 in
+// fp32, so no inf/inf; b = inf (y < -88) gives the correct 0.
+__device__ __forceinline__ float gated_product_scaled(float ax, float by) {
+    ax = fminf(fmaxf(ax, -43.280851226668903f), 43.280851226668903f);
+    const float a = __builtin_amdgcn_exp2f(ax);
+    const float b = __builtin_amdgcn_exp2f(by);
+    const float ia = 1.0f + a;
+    return (1.0f - a) * __builtin_amdgcn_rcpf(fmaf(ia, b, ia));
 }
 
+constexpr float kM2Log2e = -2.8853900817779268f;   // -2 / ln 2
+constexpr float kMLog2e = -1.4426950408889634f;    // -1 / ln 2
+
 // Fold the gate pairs of one pass into per-lane partial scores. acc[rt][2j] / acc[rt][2j+1]
-// hold V / U pre-activations of pair q0 + j for instance rt*16 + (lane & 15) and
-// d = 16*db + 4*(lane >> 4) + v (16x16 C layout with the weights as the A operand).
-template <int RT, int PPW, int MAXC>
+// hold V / U pre-activations (before the dropout scale) of pair q0 + j for instance
+// rt*16 + (lane & 15) and d = 16*db + 4*(lane >> 4) + v (16x16 C layout, weights as A).
+// ONE_CLASS: every pair of this wave belongs to gate g and feeds class g only (separate
+// heads): one accumulator, part[0]. Otherwise part[c] for every class (shared gate).
+template <int RT, int PPW, int MAXC, bool ONE_CLASS>
 __device__ __forceinline__ void fold_pairs(const GateParams& p, const f32x4 (&acc)[RT][2 * PPW],
                                            int q0, int lane, float (&part)[MAXC][RT]) {
     const int DB = p.D >> 4;
+    const float av_s = p.sf * kM2Log2e, au_s = p.sf * kMLog2e;
 #pragma unroll
     for (int jp = 0; jp < PPW; ++jp) {
         const int q = q0 + jp;
         if (q >= p.P) break;
         const int g = q / DB, db = q - g * DB;
         const int d0 = db * 16 + 4 * (lane >> 4);
-        const f32x4 bvv = *reinterpret_cast<const f32x4*>(p.bv + (size_t)g * p.D + d0);
-        const f32x4 buv = *reinterpret_cast<const f32x4*>(p.bu + (size_t)g * p.D + d0);
+        f32x4 bvv = *reinterpret_cast<const f32x4*>(p.bv + (size_t)g * p.D + d0);
+        f32x4 buv = *reinterpret_cast<const f32x4*>(p.bu + (size_t)g * p.D + d0);
+        bvv *= kM2Log2e;
+        buv *= kMLog2e;
         f32x4 coef[MAXC];
 #pragma unroll
         for (int c = 0; c < MAXC; ++c) {
-            const bool use = (c < p.C) && (p.G == 1 || c == g);
+            const int cc = ONE_CLASS ? g : c;
+            const bool use = ONE_CLASS ? (c == 0) : ((c < p.C) && (p.G == 1 || c == g));
             // address stays inside wa[C, D] for every c; unused classes get 0
-            const f32x4 w = *reinterpret_cast<const f32x4*>(p.wa + (size_t)(use ? c : 0) * p.D + d0);
+            const f32x4 w = *reinterpret_cast<const f32x4*>(p.wa + (size_t)(use ? cc : 0) * p.D + d0);
             coef[c] = use ? w : f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-                const float pr = gated_product(fmaf(acc[rt][2 * jp][v], p.sf, bvv[v]),
-                                               fmaf(acc[rt][2 * jp + 1][v], p.sf, buv[v]));
+                const float pr = gated_product_scaled(fmaf(acc[rt][2 * jp][v], av_s, bvv[v]),
+                                                      fmaf(acc[rt][2 * jp + 1][v], au_s, buv[v]));
+                if constexpr (ONE_CLASS) {
+                    part[0][rt] = fmaf(pr, coef[0][v], part[0][rt]);
+                } else {
 #pragma unroll
-                for (int c = 0; c < MAXC; ++c) part[c][rt] = fmaf(pr, coef[c][v], part[c][rt]);
+                    for (int c = 0; c < MAXC; ++c) part[c][rt] = fmaf(pr, coef[c][v], part[c][rt]);
+                }
             }
         }
     }
@@ -120,18 +135,19 @@ __device__ __forceinline__ void fold_pairs(const GateParams& p, const f32x4 (&ac
 
 // Cross-wave reduction of the partial scores + attention bias, logit dropout and stores
 // (model.py:289-291 / 299-301); z = sf * (X . k_c) for the classifier (model.py:313-315).
+// one_class >= 0: part[0] holds the wave's scores for class one_class (other classes 0).
 template <int BM, int MAXC>
 __device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
                                               float (&part)[MAXC][BM / 16], f32x4 zacc,
                                               bool zwave, float* red, float* zred,
-                                              const int* rinfo) {
+                                              const int* rinfo, int one_class = -1) {
     constexpr int RT = BM / 16;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c)
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
-            float v = part[c][rt];
+            float v = one_class < 0 ? part[c][rt] : (c == one_class ? part[0][rt] : 0.f);
             v += __shfl_xor(v, 16);
             v += __shfl_xor(v, 32);
             if (lane < 16) red[(wave * MAXC + c) * BM + rt * 16 + lane] = v;
@@ -204,6 +220,35 @@ __device__ __forceinline__ void store_masked(const Raw<float>& h, uint32_t kb, f
     *reinterpret_cast<f32x4*>(dst + 4) = b;
 }
 
+// Stage 8 features with the keep rule applied straight to the Philox words (2 draws each).
+__device__ __forceinline__ void store_dropped(const Raw<__bf16>& h, uint4 o, uint32_t thrx,
+                                              uint32_t inval, __bf16* dst) {
+    uint4 v = h.v;
+    v.x &= ~(drop_mask16x2(o.x, thrx) | inval);
+    v.y &= ~(drop_mask16x2(o.y, thrx) | inval);
+    v.z &= ~(drop_mask16x2(o.z, thrx) | inval);
+    v.w &= ~(drop_mask16x2(o.w, thrx) | inval);
+    *reinterpret_cast<uint4*>(dst) = v;
+}
+__device__ __forceinline__ uint32_t keep_lo(uint32_t m) { return ~(uint32_t)((int32_t)(m << 16) >> 16); }
+__device__ __forceinline__ uint32_t keep_hi(uint32_t m) { return ~(uint32_t)((int32_t)m >> 16); }
+__device__ __forceinline__ void store_dropped(const Raw<float>& h, uint4 o, uint32_t thrx,
+                                              uint32_t inval, float* dst) {
+    const uint32_t m0 = drop_mask16x2(o.x, thrx) | inval, m1 = drop_mask16x2(o.y, thrx) | inval;
+    const uint32_t m2 = drop_mask16x2(o.z, thrx) | inval, m3 = drop_mask16x2(o.w, thrx) | inval;
+    f32x4 a = h.lo, b = h.hi;
+    a.x = __uint_as_float(__float_as_uint(a.x) & keep_lo(m0));
+    a.y = __uint_as_float(__float_as_uint(a.y) & keep_hi(m0));
+    a.z = __uint_as_float(__float_as_uint(a.z) & keep_lo(m1));
+    a.w = __uint_as_float(__float_as_uint(a.w) & keep_hi(m1));
+    b.x = __uint_as_float(__float_as_uint(b.x) & keep_lo(m2));
+    b.y = __uint_as_float(__float_as_uint(b.y) & keep_hi(m2));
+    b.z = __uint_as_float(__float_as_uint(b.z) & keep_lo(m3));
+    b.w = __uint_as_float(__float_as_uint(b.w) & keep_hi(m3));
+    *reinterpret_cast<f32x4*>(dst) = a;
+    *reinterpret_cast<f32x4*>(dst + 4) = b;
+}
+
 constexpr int kPipeBM = 128;
 
 template <typename E, int MAXC>
@@ -212,7 +257,7 @@ __host__ __device__ constexpr size_t pipe_lds_bytes() {
            (size_t)MAXC * kPipeBM * 4 + (size_t)kRowInfo * kPipeBM * 4;
 }
 
-template <typename E, int PPW, int MAXC, bool REPLAY>
+template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS>
 __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int BM = kPipeBM;
@@ -243,16 +288,16 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     const uint8_t* kfe = REPLAY ? p.keep_feat + (size_t)(valid ? R0 + wave * 16 + (lane & 15) : 0) *
                                                     (p.L >> 3) + kq
                                 : nullptr;
-    const uint32_t vmask = valid ? 0xFFu : 0u;
 
+    const uint32_t inval = valid ? 0u : 0xFFFFFFFFu;   // padding rows stage zeros
     auto stage = [&](int s, const Raw<E>& h, E* slot) {
-        uint32_t kb;
         if constexpr (REPLAY) {
-            kb = kfe[(size_t)(s < KS ? s : KS - 1) * 4];   // step KS is a dummy: stay in the row
+            const uint32_t kb = kfe[(size_t)(s < KS ? s : KS - 1) * 4];  // step KS: dummy, in-row
+            store_masked(h, kb & ~inval, slot + tid * 8);
         } else {
-            kb = keep_byte(philox4x32_10((uint32_t)(s * 4 + kq), cn, ct, cb, p.k0, p.k1), p.thr_f);
+            const uint4 o = philox4x32_10((uint32_t)(s * 4 + kq), cn, ct, cb, p.k0, p.k1);
+            store_dropped(h, o, p.thrx_f, inval, slot + tid * 8);
         }
-        store_masked(h, kb & vmask, slot + tid * 8);
     };
 
     // weight tiles of this wave (idle pair slots read a valid tile; fold_pairs skips them)
@@ -321,8 +366,10 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     for (int c = 0; c < MAXC; ++c)
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) part[c][rt] = 0.f;
-    fold_pairs<RT, PPW, MAXC>(p, acc, q0, lane, part);
-    finish_scores<BM, MAXC>(p, R0, part, zacc, true, red, zred, rinfo);
+    fold_pairs<RT, PPW, MAXC, ONE_CLASS>(p, acc, q0, lane, part);
+    // ONE_CLASS: the wave's pairs all belong to gate q0 / (D/16) (idle waves: class >= C)
+    const int one_class = ONE_CLASS ? (q0 < p.P ? q0 / (p.D >> 4) : MAXC) : -1;
+    finish_scores<BM, MAXC>(p, R0, part, zacc, true, red, zred, rinfo, one_class);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -449,7 +496,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_scores_kernel(const GatePar
             zcur = znxt;
         }
         if (!active) continue;
-        fold_pairs<RT, PPW, MAXC>(p, acc, q0, lane, part);
+        fold_pairs<RT, PPW, MAXC, false>(p, acc, q0, lane, part);
     }
     finish_scores<BM, MAXC>(p, R0, part, zacc, zwave, red, zred, rinfo);
 }
