@@ -102,6 +102,8 @@ typedef struct mcgmil_args {
     /* ---- scratch ---- */
     void* workspace;      /* >= mcgmil_workspace_size() bytes, 256-byte aligned */
     size_t workspace_bytes;
+    void* debug;          /* diagnostic builds only (-DMCGMIL_STAMPS): per-tile s_memtime
+                             stamps; ignored by the product build. NULL otherwise */
 } mcgmil_args;
 
 int mcgmil_abi_version(void);

@@ -256,6 +256,7 @@ int mcgmil_gate_scores(const mcgmil_args* a, void* stream) {
     gp.keep_att = a->keep_att;
     gp.logits = reinterpret_cast<float*>(static_cast<char*>(a->workspace) + l.logits_off);
     gp.zz = reinterpret_cast<float*>(static_cast<char*>(a->workspace) + l.zz_off);
+    gp.stamps = static_cast<unsigned long long*>(a->debug);
 
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (a->h_dtype == MCGMIL_BF16) return dispatch_gate<__bf16>(gp, a->L, a->h_dtype, s);

@@ -40,7 +40,22 @@ struct GateParams {
     const uint8_t* keep_att;
     float* logits;                 // [T*total_rows, C]
     float* zz;                     // [T*total_rows, C]
+    unsigned long long* stamps;    // diagnostic build only: [tiles][8] s_memtime stamps
 };
+
+// In-kernel phase stamps (diagnostic build, -DMCGMIL_STAMPS; compiled out otherwise): lane 0
+// of wave 0 records s_memtime into stamps[tile * 8 + i].
+#ifdef MCGMIL_STAMPS
+#define MCGMIL_STAMP(p, i)                                                                 \
+    do {                                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        if (threadIdx.x == 0 && (p).stamps)                                                 \
+            (p).stamps[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime();        \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+    } while (0)
+#else
+#define MCGMIL_STAMP(p, i) do {} while (0)
+#endif
 
 constexpr int kGateThreads = 512;  // 8 waves
 constexpr int kGateWaves = kGateThreads / kWave;
@@ -135,49 +150,67 @@ __device__ __forceinline__ void fold_pairs(const GateParams& p, const f32x4 (&ac
 
 // Cross-wave reduction of the partial scores + attention bias, logit dropout and stores
 // (model.py:289-291 / 299-301); z = sf * (X . k_c) for the classifier (model.py:313-315).
+// Partial scores in LDS: red[wave][class][lane group g = lane >> 4][rt][instance r16 = lane & 15]
+// -- no cross-lane shuffles; with the instance fastest, both the stores (one per rt) and the
+// scoring thread's reads (it sums the 4 lane groups of every wave holding its class) are
+// bank-conflict free.
+template <int BM, int MAXC>
+__host__ __device__ constexpr int red_floats() { return kGateWaves * MAXC * 64 * (BM / 16); }
+
 // one_class >= 0: part[0] holds the wave's scores for class one_class (other classes 0).
+// Output item of a thread: row wave*16 + (lane & 15), class lane >> 4 (C <= 4) -- the (row,
+// class) whose attention-dropout draw the pipelined kernel may already have made in its K
+// loop (have_keep, keep); otherwise it is drawn here.
 template <int BM, int MAXC>
 __device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
                                               float (&part)[MAXC][BM / 16], f32x4 zacc,
                                               bool zwave, float* red, float* zred,
-                                              const int* rinfo, int one_class = -1) {
+                                              const int* rinfo, int one_class, int waves_per_gate,
+                                              bool have_keep, bool keep) {
     constexpr int RT = BM / 16;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ncls = one_class < 0 ? MAXC : 1;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
+    for (int c = 0; c < MAXC; ++c) {
+        if (c >= ncls) break;
+        const int cls = one_class < 0 ? c : one_class;
+        if (cls >= MAXC) break;                       // idle wave (no pairs)
+        float* dst = red + ((size_t)(wave * MAXC + cls) * 4 + (lane >> 4)) * (16 * RT) + (lane & 15);
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-            float v = one_class < 0 ? part[c][rt] : (c == one_class ? part[0][rt] : 0.f);
-            v += __shfl_xor(v, 16);
-            v += __shfl_xor(v, 32);
-            if (lane < 16) red[(wave * MAXC + c) * BM + rt * 16 + lane] = v;
-        }
+        for (int q = 0; q < RT; ++q) dst[16 * q] = part[c][q];
+    }
     if (zwave && lane < 16) {
 #pragma unroll
         for (int c = 0; c < MAXC; ++c) zred[c * BM + wave * 16 + lane] = zacc[c];
     }
+    MCGMIL_STAMP(p, 5);
     __syncthreads();
-    for (int i = tid; i < BM * p.C; i += kGateThreads) {
-        const int c = i / BM, r = i - c * BM;
-        const int* ri = rinfo + kRowInfo * r;
-        if (ri[0] < 0) continue;
-        float s = 0.f;
-#pragma unroll
-        for (int w = 0; w < kGateWaves; ++w) s += red[(w * MAXC + c) * BM + r];
-        s += p.ba[c];
-        const int t = ri[1], n = ri[2], bag = ri[3], Nb = ri[4];
-        bool keep;
-        if (p.keep_att) {
-            const size_t abase = (size_t)p.T * p.C * (size_t)p.bag_off[bag];
-            keep = p.keep_att[abase + ((size_t)t * p.C + c) * Nb + n] != 0;
-        } else {
-            keep = attention_keep(p.k0, p.k1, (uint32_t)ri[5], (uint32_t)(p.t_base + t),
-                                  (uint32_t)c, (uint32_t)n, p.thr_a);
-        }
-        const size_t o = (size_t)(R0 + r) * p.C + c;
-        p.logits[o] = s * (keep ? p.sa : 0.f);
-        p.zz[o] = zred[c * BM + r] * p.sf;
+    MCGMIL_STAMP(p, 6);
+    const int r = wave * 16 + (lane & 15), c = lane >> 4;
+    if (r >= BM || c >= p.C) return;
+    const int* ri = rinfo + kRowInfo * r;
+    if (ri[0] < 0) return;
+    // waves holding class c: every wave (waves_per_gate = 0: shared gate) or, one class per
+    // wave, the waves w with w / waves_per_gate == c (their other slots are never written)
+    float s = 0.f;
+    const int nw = waves_per_gate ? waves_per_gate : kGateWaves;
+    for (int k = 0; k < nw; ++k) {
+        const int w = waves_per_gate ? c * waves_per_gate + k : k;
+        const float* src = red + (size_t)(w * MAXC + c) * 4 * (16 * RT) + r;   // r = rt*16 + r16
+        s += (src[0] + src[16 * RT]) + (src[32 * RT] + src[48 * RT]);
     }
+    s += p.ba[c];
+    const int t = ri[1], n = ri[2], bag = ri[3], Nb = ri[4];
+    if (p.keep_att) {
+        const size_t abase = (size_t)p.T * p.C * (size_t)p.bag_off[bag];
+        keep = p.keep_att[abase + ((size_t)t * p.C + c) * Nb + n] != 0;
+    } else if (!have_keep) {
+        keep = attention_keep(p.k0, p.k1, (uint32_t)ri[5], (uint32_t)(p.t_base + t), (uint32_t)c,
+                              (uint32_t)n, p.thr_a);
+    }
+    const size_t o = (size_t)(R0 + r) * p.C + c;
+    p.logits[o] = s * (keep ? p.sa : 0.f);
+    p.zz[o] = zred[c * BM + r] * p.sf;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -250,10 +283,21 @@ __device__ __forceinline__ void store_dropped(const Raw<float>& h, uint4 o, uint
 }
 
 constexpr int kPipeBM = 128;
+#ifndef MCGMIL_VPM
+#define MCGMIL_VPM 2
+#endif
+constexpr int VPM = MCGMIL_VPM;   // VALU instructions scheduled after each MFMA in a K step
+#ifndef MCGMIL_SCHED
+#define MCGMIL_SCHED 0
+#endif
+#ifndef MCGMIL_ATT_IN_LOOP
+#define MCGMIL_ATT_IN_LOOP 0        // 1: draw the attention-logit keep in the K loop's last
+                                    // step (measured slower: 790 vs 825 TFLOP/s)
+#endif
 
 template <typename E, int MAXC>
 __host__ __device__ constexpr size_t pipe_lds_bytes() {
-    return (size_t)2 * kPipeBM * 32 * sizeof(E) + (size_t)kGateWaves * MAXC * kPipeBM * 4 +
+    return (size_t)2 * kPipeBM * 32 * sizeof(E) + (size_t)red_floats<kPipeBM, MAXC>() * 4 +
            (size_t)MAXC * kPipeBM * 4 + (size_t)kRowInfo * kPipeBM * 4;
 }
 
@@ -269,12 +313,14 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
 
     E* Xs = reinterpret_cast<E*>(smem);                                   // [2][SLOT]
     float* red = reinterpret_cast<float*>(smem + (size_t)2 * SLOT * sizeof(E));
-    float* zred = red + kGateWaves * MAXC * BM;
+    float* zred = red + red_floats<BM, MAXC>();
     int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);
     const long long R0 = (long long)blockIdx.x * BM;
 
+    MCGMIL_STAMP(p, 0);
     fill_row_table<BM>(p, R0, rinfo);
     __syncthreads();
+    MCGMIL_STAMP(p, 1);
 
     // staging item of this thread: row wave*16 + (lane & 15), 8-chunk kq = lane >> 4 of
     // every K step; it lands at lane slot `lane` of row tile `wave` (= element tid*8)
@@ -290,13 +336,20 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
                                 : nullptr;
 
     const uint32_t inval = valid ? 0u : 0xFFFFFFFFu;   // padding rows stage zeros
+    // The staging of step KS is never read (idle slot); its Philox call draws this thread's
+    // attention-logit keep instead: (row, class kq), counter {n>>3, c, t | 2^31, bag}.
+    bool akeep = true;
     auto stage = [&](int s, const Raw<E>& h, E* slot) {
         if constexpr (REPLAY) {
             const uint32_t kb = kfe[(size_t)(s < KS ? s : KS - 1) * 4];  // step KS: dummy, in-row
             store_masked(h, kb & ~inval, slot + tid * 8);
         } else {
-            const uint4 o = philox4x32_10((uint32_t)(s * 4 + kq), cn, ct, cb, p.k0, p.k1);
+            const bool att = MCGMIL_ATT_IN_LOOP && s == KS;
+            const uint4 o = philox4x32_10(att ? (cn >> 3) : (uint32_t)(s * 4 + kq),
+                                          att ? (uint32_t)kq : cn,
+                                          att ? (ct | 0x80000000u) : ct, cb, p.k0, p.k1);
             store_dropped(h, o, p.thrx_f, inval, slot + tid * 8);
+            akeep = att ? draw_u16(o, (int)(cn & 7u)) >= p.thr_a : akeep;
         }
     };
 
@@ -342,6 +395,33 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
         const Frag<E> xz = load_frag(cur + (size_t)tid * 8);  // row tile `wave`
         zacc = mma(z, xz, zacc);
         stage(s + 1, h, nxt);           // step KS is staged into the idle slot and never read
+        if constexpr (sizeof(E) == 2 && PPW == 2) {
+            // Spread the Philox/staging VALU over the MFMA stream (1 MFMA : VPM VALU) instead
+            // of one block after it: the two waves of a SIMD run the step in lockstep, so a
+            // trailing VALU block would not overlap the partner's MFMAs.
+#if MCGMIL_SCHED == 1
+            // + the global prefetches first and the LDS operand reads two row tiles ahead
+            __builtin_amdgcn_sched_group_barrier(0x020, NJ + 2, 0);  // VMEM reads (W, z, H)
+            __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);       // DS reads x0, x1, xz
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
+                }
+                if (rt + 2 < RT) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // z
+            __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
+#else
+#pragma unroll
+            for (int i = 0; i < RT * NJ + 1; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0); // VALU
+            }
+#endif
+        }
         __syncthreads();
     };
 
@@ -355,11 +435,13 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     for (int j = 0; j < NJ; ++j) wA[j] = load_frag(wbase[j]);
     zA = load_frag(zbase);
     __syncthreads();
+    MCGMIL_STAMP(p, 2);
 
     for (int s = 0; s < KS; s += 2) {     // KS is even (host guarantees L % 64 == 0)
         kstep(s, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA);
         kstep(s + 1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB);
     }
+    MCGMIL_STAMP(p, 3);
 
     float part[MAXC][RT];
 #pragma unroll
@@ -367,9 +449,12 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) part[c][rt] = 0.f;
     fold_pairs<RT, PPW, MAXC, ONE_CLASS>(p, acc, q0, lane, part);
+    MCGMIL_STAMP(p, 4);
     // ONE_CLASS: the wave's pairs all belong to gate q0 / (D/16) (idle waves: class >= C)
     const int one_class = ONE_CLASS ? (q0 < p.P ? q0 / (p.D >> 4) : MAXC) : -1;
-    finish_scores<BM, MAXC>(p, R0, part, zacc, true, red, zred, rinfo, one_class);
+    finish_scores<BM, MAXC>(p, R0, part, zacc, true, red, zred, rinfo, one_class,
+                            ONE_CLASS ? (p.D >> 4) / PPW : 0, !REPLAY && MCGMIL_ATT_IN_LOOP, akeep);
+    MCGMIL_STAMP(p, 7);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -381,8 +466,9 @@ __host__ __device__ constexpr int gate_row_info_ints() { return kRowInfo * BM; }
 
 template <typename E, int BM, int MAXC>
 __host__ __device__ constexpr size_t gate_lds_bytes(int L) {
-    return (size_t)BM * L * sizeof(E) + (size_t)kGateWaves * MAXC * BM * 4 + (size_t)MAXC * BM * 4 +
-           (size_t)gate_row_info_ints<BM>() * 4;
+    // the partial scores alias the masked tile once every pass is done (see the kernel)
+    const size_t tile = (size_t)BM * L * sizeof(E), red = (size_t)red_floats<BM, MAXC>() * 4;
+    return (tile > red ? tile : red) + (size_t)MAXC * BM * 4 + (size_t)gate_row_info_ints<BM>() * 4;
 }
 
 template <typename E, int BM, int PPW, int MAXC>
@@ -398,8 +484,9 @@ __global__ __launch_bounds__(kGateThreads) void gate_scores_kernel(const GatePar
     const int LC = L >> 3;
 
     E* Xs = reinterpret_cast<E*>(smem);
-    float* red = reinterpret_cast<float*>(smem + (size_t)BM * L * sizeof(E));
-    float* zred = red + kGateWaves * MAXC * BM;
+    float* red = reinterpret_cast<float*>(smem);     // aliases Xs after the last pass
+    const size_t tile_bytes = (size_t)BM * L * sizeof(E), red_bytes = (size_t)red_floats<BM, MAXC>() * 4;
+    float* zred = reinterpret_cast<float*>(smem + (tile_bytes > red_bytes ? tile_bytes : red_bytes));
     int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);
     const long long R0 = (long long)blockIdx.x * BM;
 
@@ -498,7 +585,8 @@ __global__ __launch_bounds__(kGateThreads) void gate_scores_kernel(const GatePar
         if (!active) continue;
         fold_pairs<RT, PPW, MAXC, false>(p, acc, q0, lane, part);
     }
-    finish_scores<BM, MAXC>(p, R0, part, zacc, zwave, red, zred, rinfo);
+    __syncthreads();   // every wave is done reading Xs: `red` may overwrite it
+    finish_scores<BM, MAXC>(p, R0, part, zacc, zwave, red, zred, rinfo, -1, 0, false, true);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -16,26 +16,29 @@ DEPS = ["mcgmil.hip", "mcgmil_kernels.h", "mcgmil_device.h"]
 ARCH = os.environ.get("MCGMIL_OFFLOAD_ARCH", "gfx950")
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def _stale(out: str = LIB) -> bool:
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(out)
     deps = [os.path.join(CSRC, d) for d in DEPS] + [os.path.join(INCLUDE, "mcgmil.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
-        return LIB
+def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()) -> str:
+    """Build libmcgmil.so (or, with defines such as MCGMIL_STAMPS, a diagnostic variant at
+    `out`)."""
+    if not force and not _stale(out):
+        return out
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall",
-           "-Werror", f"-I{INCLUDE}", "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+           "-Werror", f"-I{INCLUDE}", "-o", tmp] + [f"-D{d}" for d in defines] + \
+          [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

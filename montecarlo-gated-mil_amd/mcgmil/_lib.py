@@ -40,7 +40,7 @@ class Args(ctypes.Structure):
         ("bag_id_base", ctypes.c_uint32), ("t_base", ctypes.c_int32), ("bag_ids", _vp),
         ("keep_feat", _vp), ("keep_att", _vp),
         ("Y", _vp), ("A", _vp), ("A_mean", _vp), ("A_var", _vp), ("P_mean", _vp),
-        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t), ("debug", _vp),
     ]
 
 

@@ -32,6 +32,9 @@ for s in $STEPS; do
         tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
         bench) run bench 600 python bench.py ;;
         probe) run probe 300 python scripts/probe_gate.py ;;
+        stamps) run stamps 300 python scripts/probe_stamps.py ;;
+        ab) run ab 300 env MCGMIL_PROBE_LIBS="$(ls -1 /tmp/mcgmil_var/*.so 2>/dev/null | paste -sd, -)" \
+                PROBE_ONLY=philox python scripts/probe_gate.py ;;
         prof)
             rm -rf "$OUT/prof_$TAG"
             run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run \

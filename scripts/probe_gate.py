@@ -18,22 +18,36 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
 
+def load_variant(path):
+    L = ctypes.CDLL(path)
+    for f in ("mcgmil_gate_scores", "mcgmil_workspace_size"):
+        getattr(L, f).restype = ctypes.c_int
+    return L
+
+
 def main():
     from mcgmil import _lib, ops
     from oracle import synthetic
-    lib = _lib.load()
+    _lib.load()
+    # MCGMIL_PROBE_LIBS=a.so,b.so: A/B variant builds of the library in one process
+    paths = [p for p in os.environ.get("MCGMIL_PROBE_LIBS", "").split(",") if p]
+    libs = {os.path.basename(p): load_variant(p) for p in paths} or {"libmcgmil.so": _lib.load()}
+    only = os.environ.get("PROBE_ONLY", "")
     dev = torch.device("cuda", 0)
     N, T, L, D, C = 2048, 100, 512, 128, 2
     B = int(os.environ.get("PROBE_BAGS", "16"))
     rounds = int(os.environ.get("PROBE_ROUNDS", "7"))
     iters = 5
     variants = []
-    for dtype in (torch.bfloat16, torch.float32):
-        for shared in (False, True):
-            for mode in ("philox", "replay", "p0"):
-                if dtype == torch.float32 and mode != "philox":
-                    continue
-                variants.append((dtype, shared, mode))
+    for name in libs:
+        for dtype in (torch.bfloat16, torch.float32):
+            for shared in (False, True):
+                for mode in ("philox", "replay", "p0"):
+                    if dtype == torch.float32 and mode != "philox":
+                        continue
+                    if only and mode not in only.split(","):
+                        continue
+                    variants.append((name, dtype, shared, mode))
     setups = {}
     g = torch.Generator(device=dev).manual_seed(0)
     Hf = torch.randn(B * N, L, device=dev, generator=g).abs_()
@@ -42,7 +56,7 @@ def main():
     sh = ctypes.c_void_p(stream.cuda_stream)
     keep_f = keep_a = None
     for v in variants:
-        dtype, shared, mode = v
+        name, dtype, shared, mode = v
         G = 1 if shared else C
         Bv = B if dtype == torch.bfloat16 else max(1, B // 4)
         H = Hf[:Bv * N].to(dtype).contiguous()
@@ -60,15 +74,16 @@ def main():
             a.keep_feat = ctypes.c_void_p(keep_f.data_ptr())
             a.keep_att = ctypes.c_void_p(keep_a.data_ptr())
         n = ctypes.c_size_t()
+        lib = libs[name]
         _lib.check(lib.mcgmil_workspace_size(ctypes.byref(a), ctypes.byref(n)), "ws")
         ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
         a.workspace, a.workspace_bytes = ctypes.c_void_p(ws.data_ptr()), n.value
         flops = Bv * T * (2 * N * L * D * 2 * G + 2 * N * D * C + 2 * N * L * C + 2 * L * C)
-        setups[v] = (a, ws, H, head, packed, flops, Bv)
+        setups[v] = (a, ws, H, head, packed, flops, Bv, lib)
     times = {v: [] for v in variants}
     for _ in range(rounds):
         for v in variants:
-            a = setups[v][0]
+            a, lib = setups[v][0], setups[v][7]
             _lib.check(lib.mcgmil_gate_scores(ctypes.byref(a), sh), "gate")
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -78,10 +93,10 @@ def main():
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / iters)
     for v in variants:
-        dtype, shared, mode = v
+        name, dtype, shared, mode = v
         ms = statistics.median(times[v])
         flops, Bv = setups[v][5], setups[v][6]
-        print(json.dumps({"dtype": str(dtype).split(".")[-1], "shared": shared, "mode": mode,
+        print(json.dumps({"lib": name, "dtype": str(dtype).split(".")[-1], "shared": shared, "mode": mode,
                           "bags": Bv, "ms": round(ms, 4), "min_ms": round(min(times[v]), 4),
                           "tflops": round(flops / (ms * 1e-3) / 1e12, 1),
                           "bag_samples_per_s": round(Bv * T / (ms * 1e-3))}))

@@ -315,3 +315,42 @@ def test_unsupported_config_raises(cuda):
     with pytest.raises(_lib.MCGMILError):
         ops.mcdo_forward(H, ops.bag_offsets_tensor([8], cuda), head_on(arrays, cuda), 2,
                          p_feat=0.1, p_att=0.1, seed=0)
+
+
+# ------------------------------------------------------------------ other head shapes
+# (L, D, C, shared): which kernel instantiation each exercises
+SHAPES = [
+    (512, 128, 4, False),   # P = 32 gate tile pairs -> generic whole-tile kernel, 4 classes
+    (96, 32, 2, True),      # L % 64 != 0 -> generic kernel
+    (256, 48, 3, False),    # P = 9 -> pipelined, 2 pairs/wave spanning gates (per-class partials)
+    (1024, 64, 1, True),    # P = 4 -> pipelined, 1 pair/wave, idle waves
+    (512, 64, 3, False),    # P = 12 -> pipelined, one class per wave
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("L,D,C,shared", SHAPES)
+def test_head_shapes_match_oracle(cuda, L, D, C, shared, dtype):
+    from mcgmil import ops
+    sizes = [77, 130, 3]
+    T, seed, base = 4, 9, 5
+    sd = synthetic.head_state_dict(L + D + C, L=L, D=D, C=C, shared=shared)
+    Hs = [synthetic.bag_features(300 + b, n, L) for b, n in enumerate(sizes)]
+    if dtype == torch.bfloat16:
+        sd_ref = synthetic.round_state_dict_bf16(sd)
+        Hs_ref = [synthetic.bf16_round(h) for h in Hs]
+        tol = TOL_BF16_IN
+    else:
+        sd_ref, Hs_ref, tol = sd, Hs, TOL32
+    arrays = synthetic.head_arrays(sd, C, shared)
+    prm = mcdo_ref.HeadParams(synthetic.head_arrays(sd_ref, C, shared))
+    H = torch.from_numpy(np.concatenate(Hs)).to(cuda).to(dtype).contiguous()
+    out = ops.mcdo_forward(H, ops.bag_offsets_tensor(sizes, cuda), head_on(arrays, cuda), T,
+                           p_feat=0.2, p_att=0.1, seed=seed, bag_id_base=base, return_stats=True)
+    Y = out["Y"].cpu().numpy()
+    A = ops.split_bags(out["A"].cpu(), sizes, T * C)
+    for b, n in enumerate(sizes):
+        kF, kA = mcdo_ref.masks_for_bag(seed, base + b, T, n, L, C, 0.2, 0.1)
+        Yr, Ar = mcdo_ref.mc_inference(Hs_ref[b], prm, kF, kA, 0.2, 0.1)
+        np.testing.assert_allclose(Y[b], Yr[:, 0].numpy(), atol=tol["Y"])
+        assert nrel(A[b].numpy().reshape(T, C, n), Ar[:, 0].numpy()) <= tol["A"]
