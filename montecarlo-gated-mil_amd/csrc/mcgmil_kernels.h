@@ -287,6 +287,9 @@ constexpr int kPipeBM = 128;
 #define MCGMIL_VPM 2
 #endif
 constexpr int VPM = MCGMIL_VPM;   // VALU instructions scheduled after each MFMA in a K step
+#ifndef MCGMIL_DIAG
+#define MCGMIL_DIAG 0               // ablation bits for timing studies (never in the product)
+#endif
 #ifndef MCGMIL_SCHED
 #define MCGMIL_SCHED 0
 #endif
@@ -345,9 +348,13 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
             store_masked(h, kb & ~inval, slot + tid * 8);
         } else {
             const bool att = MCGMIL_ATT_IN_LOOP && s == KS;
+#if MCGMIL_DIAG & 4   // ablation: no Philox (keep pattern from the counters)
+            const uint4 o = make_uint4(cn * 0x9E3779B9u + (uint32_t)s, ct ^ cb, cn + ct, (uint32_t)s * 77u);
+#else
             const uint4 o = philox4x32_10(att ? (cn >> 3) : (uint32_t)(s * 4 + kq),
                                           att ? (uint32_t)kq : cn,
                                           att ? (ct | 0x80000000u) : ct, cb, p.k0, p.k1);
+#endif
             store_dropped(h, o, p.thrx_f, inval, slot + tid * 8);
             akeep = att ? draw_u16(o, (int)(cn & 7u)) >= p.thr_a : akeep;
         }
@@ -382,10 +389,20 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
                      Frag<E> (&wn)[NJ], Frag<E>& zn, const Raw<E>& h, Raw<E>& hn) {
         const int s1 = s + 1 < KS ? s + 1 : KS - 1;          // clamped: no branch in the body
         const int s2 = s + 2 < KS ? s + 2 : KS - 1;
+#if MCGMIL_DIAG & 1   // ablation (timing only, wrong results): no H prefetch
+        hn = h;
+#else
         hn = load_raw(hsrc + (size_t)s2 * 32);
+#endif
+#if MCGMIL_DIAG & 2   // ablation: no weight prefetch
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) wn[j] = w[j];
+        zn = z;
+#else
 #pragma unroll
         for (int j = 0; j < NJ; ++j) wn[j] = load_frag(wbase[j] + (size_t)s1 * 512);
         zn = load_frag(zbase + (size_t)s1 * 512);
+#endif
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
             const Frag<E> x = load_frag(cur + (size_t)(rt * 64 + lane) * 8);
