@@ -43,6 +43,18 @@ def bytes_per_bag(N, T, L, C, esize):
     return N * L * esize + 4 * T * C * N + 4 * T * C
 
 
+def measured_traffic(N, T, B, dtype, shared):
+    """HBM bytes per gate launch from the committed rocprofv3 PMC passes (profiles/*/
+    gate_traffic.json, newest round first) when they were taken on this exact workload."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "gate_traffic.json")),
+                       reverse=True):
+        t = json.load(open(path))
+        if t.get("config") == {"bags": B, "N": N, "T": T, "dtype": dtype, "shared": shared}:
+            return t["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
+    return None, None
+
+
 def cpu_baseline(N, T, L, D, C, shared, budget_s):
     """The reference CPU path (torch op sequence incl. dropout RNG), bounded sample."""
     from oracle import mcdo_ref, synthetic
@@ -162,6 +174,7 @@ def main():
     achieved = F / (gate_ms * 1e-3) / 1e12
     hbm_bytes = bytes_per_bag(N, T, L, C, esize) * B + packed.numel()
     hbm_gbs = hbm_bytes / (gate_ms * 1e-3) / 1e9
+    traffic, traffic_src = measured_traffic(N, T, B, args.dtype, args.shared)
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(N, T, L, D, C, bool(args.shared),
                                                              args.cpu_budget)
@@ -177,7 +190,8 @@ def main():
                        "N": N, "L": L, "D": D, "C": C, "T": T, "parallelism": f"bags over {world} GPU(s)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[args.dtype],
                          "unit": "TFLOP/s", "frac": achieved / PEAK_TFLOPS[args.dtype],
-                         "traffic": None, "kernel": "gate_scores_kernel",
+                         "traffic": traffic, "traffic_unit": "HBM bytes per launch",
+                         "traffic_source": traffic_src, "kernel": "gate_pipe_kernel",
                          "kernel_ms": gate_ms, "algorithmic_tflop_per_launch": F / 1e12},
             "roofline_hbm": {"achieved": hbm_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": hbm_gbs / PEAK_HBM_GBS,

@@ -41,6 +41,14 @@ for s in $STEPS; do
                 --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
             find "$OUT/prof_$TAG" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_$TAG.csv" \;
             ;;
+        pmc)
+            for ctr in FETCH_SIZE WRITE_SIZE; do
+                rm -rf "$OUT/pmc_${TAG}_$ctr"
+                run pmc_$ctr 600 rocprofv3 --pmc $ctr --kernel-trace -d "$OUT/pmc_${TAG}_$ctr" -o run \
+                    --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline
+                find "$OUT/pmc_${TAG}_$ctr" -name "*counter_collection.csv" -exec cp {} "$OUT/pmc_${TAG}_$ctr.csv" \;
+            done
+            ;;
     esac
 done
 echo "== done"

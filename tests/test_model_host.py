@@ -1,0 +1,74 @@
+"""Host-side checks of the drop-in module (no kernel launches)."""
+import json
+import os
+
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+
+def test_head_state_dict_keys_match_reference():
+    """Reference checkpoints (model.py:182-209 parameter names/shapes) load strictly."""
+    from mcgmil import MultiHeadGatedAttentionMIL
+    ref = json.load(open(os.path.join(GOLDEN, "reference_head_keys.json")))
+    for shared, tag in ((True, "shared"), (False, "separate")):
+        m = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=shared)
+        own = {k: list(v.shape) for k, v in m.state_dict().items()
+               if not k.startswith("feature_extractor")}
+        assert own == ref[tag]
+
+
+def test_backbone_keys_follow_torchvision():
+    from mcgmil import MultiHeadGatedAttentionMIL, deactivate_batchnorm
+    m = MultiHeadGatedAttentionMIL(pretrained=False)
+    m.apply(deactivate_batchnorm)                     # infer.py:154
+    keys = set(m.state_dict())
+    for k in ("feature_extractor.conv1.weight", "feature_extractor.bn1.weight",
+              "feature_extractor.layer1.0.conv1.weight", "feature_extractor.layer2.0.downsample.0.weight",
+              "feature_extractor.layer4.1.bn2.bias", "feature_extractor.bn1.num_batches_tracked"):
+        assert k in keys, k
+    assert not any(k.endswith("running_mean") for k in keys)   # batch statistics, as infer.py
+    assert not any(k.startswith("feature_extractor.fc") for k in keys)   # fc = Identity
+
+
+def test_backbone_feature_shape_cpu():
+    """The PyTorch-ROCm feeder (not the kernel) maps 3x224x224 instances to L=512 features."""
+    from mcgmil import MultiHeadGatedAttentionMIL
+    m = MultiHeadGatedAttentionMIL(pretrained=False)
+    with torch.no_grad():
+        H = m.extract_features(torch.randn(1, 3, 3, 64, 64))
+    assert H.shape == (1, 3, 512)
+
+
+def test_pretrained_warns_offline():
+    from mcgmil import MultiHeadGatedAttentionMIL
+    with pytest.warns(UserWarning):
+        MultiHeadGatedAttentionMIL(pretrained=True, backbone="r34")
+
+
+def test_no_cpu_path():
+    from mcgmil import MultiHeadGatedAttentionMIL
+    m = MultiHeadGatedAttentionMIL(pretrained=False)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m.mc_inference(torch.zeros(1, 2, 3, 32, 32), N=2, device="cpu")
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m.mc_inference_features(torch.zeros(5, 512), T=2)
+    m.train()
+    with pytest.raises(NotImplementedError):
+        m(torch.zeros(1, 2, 3, 32, 32))
+
+
+def test_ops_reject_cpu_tensors():
+    from mcgmil import ops
+    head = ops.HeadTensors(*[torch.zeros(1, 1) for _ in range(7)])
+    with pytest.raises(ValueError):
+        ops.mcdo_forward(torch.zeros(4, 512), torch.zeros(2, dtype=torch.int32), head, 2,
+                         p_feat=0.1, p_att=0.1, seed=0)
+
+
+def test_bag_offsets_validation():
+    from mcgmil import ops
+    assert ops.bag_offsets_tensor([3, 0, 5], "cpu").tolist() == [0, 3, 3, 8]
+    with pytest.raises(ValueError):
+        ops.bag_offsets_tensor([0, 5, 3], "cpu", are_sizes=False)
