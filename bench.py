@@ -87,6 +87,11 @@ def main():
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--shared", type=int, default=0)
+    ap.add_argument("--workload", choices=["cfg3", "cfg4"], default="cfg3",
+                    help="cfg3: --bags bags of N=--n per GPU (weak scaling, the headline); "
+                         "cfg4: 4096 bags N~U(256,2048) LPT-sharded over the GPUs (strong scaling)")
+    ap.add_argument("--dist-backend", default="nccl", help=argparse.SUPPRESS)   # rehearsal: gloo
+    ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)  # ranks on cuda:0
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -95,8 +100,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+        dist.init_process_group(args.dist_backend)
+    dev = torch.device("cuda", 0 if args.same_device else local)
     torch.cuda.set_device(dev)
 
     from mcgmil import _lib, ops
@@ -105,26 +110,40 @@ def main():
 
     N, T, L, D, C = args.n, args.T, 512, 128, 2
     G = 1 if args.shared else C
-    B = args.bags
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     esize = 2 if args.dtype == "bf16" else 4
+    if args.workload == "cfg4":
+        # BASELINE config 4: 4096 bags, N_b = rng(0).integers(256, 2049, 4096), sharded LPT
+        import numpy as np
+        from mcgmil.shard import lpt_assign
+        all_sizes = np.random.default_rng(0).integers(256, 2049, 4096).tolist()
+        mine = lpt_assign([float(n) * T for n in all_sizes], world)[rank]
+        sizes = [all_sizes[b] for b in mine]
+        ids = mine
+        total_bags = len(all_sizes)
+    else:
+        sizes = [N] * args.bags
+        ids = list(range(rank * args.bags, (rank + 1) * args.bags))
+        total_bags = world * args.bags
+    B = len(sizes)
+    rows = sum(sizes)
 
     # synthetic, random-init weights of the reference architecture; features |N(0,1)|
     sd = synthetic.head_state_dict(0, L=L, D=D, C=C, shared=bool(args.shared))
     arrays = synthetic.head_arrays(sd, C, bool(args.shared))
     head = ops.HeadTensors(*[torch.from_numpy(arrays[k]).to(dev) for k in ops.HeadTensors._fields])
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    H = torch.randn(B * N, L, device=dev, generator=g).abs_().to(dt).contiguous()
-    offs = ops.bag_offsets_tensor([N] * B, dev)
-    bag_ids = torch.arange(rank * B, (rank + 1) * B, dtype=torch.int32, device=dev)
+    H = torch.randn(rows, L, device=dev, generator=g).abs_().to(dt).contiguous()
+    offs = ops.bag_offsets_tensor(sizes, dev)
+    bag_ids = torch.tensor(ids, dtype=torch.int32, device=dev)
     packed = ops.packed_weights(head, dt)
 
     a = ops.make_args(H, offs, head, T, C, G, D, 0.1, 0.1, seed=42, bag_ids=bag_ids)
     a.packed_w = ctypes.c_void_p(packed.data_ptr())
     Y = torch.empty(B, T, C, device=dev)
-    A = torch.empty(T * C * B * N, device=dev)
-    Am = torch.empty(C * B * N, device=dev)
-    Av = torch.empty(C * B * N, device=dev)
+    A = torch.empty(T * C * rows, device=dev)
+    Am = torch.empty(C * rows, device=dev)
+    Av = torch.empty(C * rows, device=dev)
     a.Y, a.A = ctypes.c_void_p(Y.data_ptr()), ctypes.c_void_p(A.data_ptr())
     a.A_mean, a.A_var = ctypes.c_void_p(Am.data_ptr()), ctypes.c_void_p(Av.data_ptr())
     n = ctypes.c_size_t()
@@ -134,7 +153,13 @@ def main():
     pa = ctypes.byref(a)
     stream = torch.cuda.current_stream(dev)
     sh = ctypes.c_void_p(stream.cuda_stream)
-    gather = [torch.empty_like(Y) for _ in range(world)] if world > 1 else None
+    if world > 1:
+        pad = torch.zeros(1, dtype=torch.int64, device=dev) + B
+        dist.all_reduce(pad, op=dist.ReduceOp.MAX)
+        Ypad = torch.zeros(int(pad), T, C, device=dev)
+        gather = [torch.empty_like(Ypad) for _ in range(world)]
+    else:
+        gather = None
 
     def step(ev=None):
         if ev is not None:
@@ -144,8 +169,9 @@ def main():
             ev[1].record(stream)
         _lib.check(lib.mcgmil_softmax_pool(pa, sh), "softmax_pool")
         _lib.check(lib.mcgmil_bag_stats(pa, sh), "bag_stats")
-        if gather is not None:
-            dist.all_gather(gather, Y)
+        if gather is not None:       # per-bag predictions to every rank (RCCL over xGMI)
+            Ypad[:B].copy_(Y)
+            dist.all_gather(gather, Ypad)
 
     for _ in range(args.warmup):
         step()
@@ -168,26 +194,32 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, gate_ms = float(t[0]), float(t[1])
 
-    total_bag_samples = world * B * T * args.steps
+    total_bag_samples = total_bags * T * args.steps
     value = total_bag_samples / el
-    F = flops_per_bag(N, T, L, D, C, G) * B
+    F = sum(flops_per_bag(n, T, L, D, C, G) for n in sizes)
     achieved = F / (gate_ms * 1e-3) / 1e12
-    hbm_bytes = bytes_per_bag(N, T, L, C, esize) * B + packed.numel()
+    hbm_bytes = sum(bytes_per_bag(n, T, L, C, esize) for n in sizes) + packed.numel()
     hbm_gbs = hbm_bytes / (gate_ms * 1e-3) / 1e9
-    traffic, traffic_src = measured_traffic(N, T, B, args.dtype, args.shared)
+    traffic, traffic_src = measured_traffic(N, T, B, args.dtype, args.shared) \
+        if args.workload == "cfg3" else (None, None)
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(N, T, L, D, C, bool(args.shared),
                                                              args.cpu_budget)
         out = {
             "metric": METRIC, "value": value, "unit": "bag-samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "weak" if args.workload == "cfg3" else "strong",
+            "vs_baseline": None,
             "dtype": args.dtype, "data": "synthetic (|N(0,1)| features, random-init head)",
-            "config": {"workload": f"BASELINE config 3: N={N} instances/bag, d={L}, D={D}, C={C}, "
-                                   f"T={T} MCDO samples, {'shared' if args.shared else 'separate'} "
-                                   f"attention, {args.dtype} operands / fp32 accumulate",
-                       "bags_per_gpu_per_step": B, "global_batch_bags": world * B,
-                       "N": N, "L": L, "D": D, "C": C, "T": T, "parallelism": f"bags over {world} GPU(s)"},
+            "config": {"workload": (f"BASELINE config 3: N={N} instances/bag" if args.workload == "cfg3"
+                                    else "BASELINE config 4: 4096 bags, N~U(256,2048)") +
+                                   f", d={L}, D={D}, C={C}, T={T} MCDO samples, "
+                                   f"{'shared' if args.shared else 'separate'} attention, "
+                                   f"{args.dtype} operands / fp32 accumulate",
+                       "bags_per_gpu_per_step": B, "global_batch_bags": total_bags,
+                       "rows_per_gpu": rows, "N": N if args.workload == "cfg3" else "U(256,2048)",
+                       "L": L, "D": D, "C": C, "T": T,
+                       "parallelism": f"bags over {world} GPU(s), LPT, RCCL all_gather of Y"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[args.dtype],
                          "unit": "TFLOP/s", "frac": achieved / PEAK_TFLOPS[args.dtype],
                          "traffic": traffic, "traffic_unit": "HBM bytes per launch",

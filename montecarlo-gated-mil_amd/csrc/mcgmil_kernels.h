@@ -150,24 +150,26 @@ __device__ __forceinline__ void fold_pairs(const GateParams& p, const f32x4 (&ac
 
 // Cross-wave reduction of the partial scores + attention bias, logit dropout and stores
 // (model.py:289-291 / 299-301); z = sf * (X . k_c) for the classifier (model.py:313-315).
-// Partial scores in LDS: red[wave][class][lane group g = lane >> 4][rt][instance r16 = lane & 15]
-// -- no cross-lane shuffles; with the instance fastest, both the stores (one per rt) and the
-// scoring thread's reads (it sums the 4 lane groups of every wave holding its class) are
-// bank-conflict free.
+// Partial scores in LDS: red[wave][class][lane group g][tile row r] -- a lane of a 16x16 (32x32)
+// accumulator holds rows r = rt*16 + (lane & 15) (rt*32 + (lane & 31)) for lane group
+// g = lane >> 4 (lane >> 5). No cross-lane shuffles; with the row fastest, the stores (one per
+// rt) and the scoring thread's reads (it sums the lane groups of every wave holding its class)
+// are bank-conflict free.
 template <int BM, int MAXC>
-__host__ __device__ constexpr int red_floats() { return kGateWaves * MAXC * 64 * (BM / 16); }
+__host__ __device__ constexpr int red_floats() { return kGateWaves * MAXC * 4 * BM; }
 
 // one_class >= 0: part[0] holds the wave's scores for class one_class (other classes 0).
 // Output item of a thread: row wave*16 + (lane & 15), class lane >> 4 (C <= 4) -- the (row,
 // class) whose attention-dropout draw the pipelined kernel may already have made in its K
 // loop (have_keep, keep); otherwise it is drawn here.
-template <int BM, int MAXC>
+template <int BM, int MAXC, int ROWS = 16>
 __device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
-                                              float (&part)[MAXC][BM / 16], f32x4 zacc,
+                                              float (&part)[MAXC][BM / ROWS], f32x4 zacc,
                                               bool zwave, float* red, float* zred,
                                               const int* rinfo, int one_class, int waves_per_gate,
                                               bool have_keep, bool keep) {
-    constexpr int RT = BM / 16;
+    constexpr int RT = BM / ROWS;
+    constexpr int NG = 64 / ROWS;                  // lane groups per accumulator tile
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ncls = one_class < 0 ? MAXC : 1;
 #pragma unroll
@@ -175,9 +177,9 @@ __device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
         if (c >= ncls) break;
         const int cls = one_class < 0 ? c : one_class;
         if (cls >= MAXC) break;                       // idle wave (no pairs)
-        float* dst = red + ((size_t)(wave * MAXC + cls) * 4 + (lane >> 4)) * (16 * RT) + (lane & 15);
+        float* dst = red + ((size_t)(wave * MAXC + cls) * NG + lane / ROWS) * BM + (lane % ROWS);
 #pragma unroll
-        for (int q = 0; q < RT; ++q) dst[16 * q] = part[c][q];
+        for (int q = 0; q < RT; ++q) dst[ROWS * q] = part[c][q];
     }
     if (zwave && lane < 16) {
 #pragma unroll
@@ -196,8 +198,9 @@ __device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
     const int nw = waves_per_gate ? waves_per_gate : kGateWaves;
     for (int k = 0; k < nw; ++k) {
         const int w = waves_per_gate ? c * waves_per_gate + k : k;
-        const float* src = red + (size_t)(w * MAXC + c) * 4 * (16 * RT) + r;   // r = rt*16 + r16
-        s += (src[0] + src[16 * RT]) + (src[32 * RT] + src[48 * RT]);
+        const float* src = red + (size_t)(w * MAXC + c) * NG * BM + r;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) s += src[g * BM];
     }
     s += p.ba[c];
     const int t = ri[1], n = ri[2], bag = ri[3], Nb = ri[4];

@@ -23,7 +23,10 @@ def main():
     from mcgmil import _build, _lib, ops
     from oracle import synthetic
     path = os.path.join(REPO, "montecarlo-gated-mil_amd", "mcgmil", "libmcgmil_stamps.so")
-    _build.build(out=path, defines=["MCGMIL_STAMPS"])   # rebuilt when stale
+    extra = [d for d in os.environ.get("STAMP_DEFINES", "").split(",") if d]
+    if extra:
+        path = path.replace(".so", "_" + "_".join(x.replace("=", "") for x in extra) + ".so")
+    _build.build(out=path, defines=["MCGMIL_STAMPS"] + extra)   # rebuilt when stale
     _lib.load()
     lib = ctypes.CDLL(path)
     for f in ("mcgmil_gate_scores", "mcgmil_workspace_size"):

@@ -325,6 +325,8 @@ SHAPES = [
     (256, 48, 3, False),    # P = 9 -> pipelined, 2 pairs/wave spanning gates (per-class partials)
     (1024, 64, 1, True),    # P = 4 -> pipelined, 1 pair/wave, idle waves
     (512, 64, 3, False),    # P = 12 -> pipelined, one class per wave
+    (512, 64, 4, False),    # G*D = 256 -> 32x32x16 kernel (bf16), 4 classes, one per 2 waves
+    (256, 256, 2, True),    # G*D = 256 -> 32x32x16 kernel (bf16), shared gate, both classes
 ]
 
 
