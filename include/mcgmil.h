@@ -68,7 +68,8 @@ typedef struct mcgmil_args {
     int64_t total_rows;   /* sum of bag sizes = rows of H (host-known) */
     /* ---- instances ---- */
     int32_t h_dtype;      /* mcgmil_dtype of H and of the GEMM operands */
-    int32_t reserved0;
+    int32_t uniform_bag_rows; /* optional hint: N if every bag has N rows (bag_offsets[b] = b*N),
+                                 0 otherwise; lets the kernels map rows to bags arithmetically */
     const void* H;        /* [total_rows, ldh] row-major; bag b = rows bag_offsets[b]..[b+1] */
     int64_t ldh;          /* row stride of H in elements (>= L) */
     const int32_t* bag_offsets; /* [B+1] CSR row offsets, bag_offsets[0] = 0 */

@@ -69,6 +69,9 @@ int validate_batch(const mcgmil_args* a) {
     if ((long long)a->T * a->total_rows > (1ll << 46)) return fail(MCGMIL_E_UNSUPPORTED, "T * total_rows too large");
     if (a->total_rows > 0x7fffffffll) return fail(MCGMIL_E_UNSUPPORTED, "total_rows must fit int32");
     if (!a->bag_offsets) return fail(MCGMIL_E_INVALID, "bag_offsets is NULL");
+    if (a->uniform_bag_rows < 0 ||
+        (a->uniform_bag_rows > 0 && (long long)a->uniform_bag_rows * a->num_bags != a->total_rows))
+        return fail(MCGMIL_E_INVALID, "uniform_bag_rows must be 0 or total_rows / num_bags");
     if (!(a->p_feat >= 0.f && a->p_feat <= 1.f) || !(a->p_att >= 0.f && a->p_att <= 1.f))
         return fail(MCGMIL_E_INVALID, "dropout probabilities must be in [0, 1]");
     return MCGMIL_OK;
@@ -76,8 +79,11 @@ int validate_batch(const mcgmil_args* a) {
 
 struct Layout {
     size_t packed_bytes;   // 0 when args->packed_w is supplied
-    size_t logits_off, zz_off, total;
+    size_t logits_off, zz_off, plan_off, total;
 };
+
+// Smallest row tile any gate kernel uses (sizes the tile plan).
+constexpr int kMinBM = 16;
 
 size_t packed_bytes_for(const mcgmil_args* a) {
     const size_t P = (size_t)a->G * (a->D / 16);
@@ -90,7 +96,9 @@ Layout layout_for(const mcgmil_args* a) {
     const size_t scores = align_up((size_t)a->T * a->total_rows * a->C * sizeof(float), 256);
     l.logits_off = l.packed_bytes;
     l.zz_off = l.logits_off + scores;
-    l.total = l.zz_off + scores;
+    l.plan_off = l.zz_off + scores;
+    const size_t max_tiles = ((size_t)a->T * a->total_rows + kMinBM - 1) / kMinBM;
+    l.total = l.plan_off + align_up(max_tiles * sizeof(int32_t), 256);
     return l;
 }
 
@@ -111,6 +119,17 @@ void raise_lds_cap(KernelT* k) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
+// The tile plan for BM-row tiles (written into the workspace; gp.tile_bag points there).
+int launch_plan(const mcgmil::GateParams& gp, int BM, hipStream_t s) {
+    const long long tiles = (gp.total_samples + BM - 1) / BM;
+    if (tiles == 0) return MCGMIL_OK;
+    hipLaunchKernelGGL(mcgmil::plan_tiles_kernel, dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0,
+                       s, gp.bag_off, gp.B, gp.T, gp.total_samples, BM, tiles,
+                       const_cast<int32_t*>(gp.tile_bag));
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "plan_tiles_kernel launch");
+}
+
 template <typename E, int BM, int PPW, int MAXC>
 int launch_gate_generic(const mcgmil::GateParams& gp, hipStream_t s) {
     auto* k = &mcgmil::gate_scores_kernel<E, BM, PPW, MAXC>;
@@ -118,6 +137,8 @@ int launch_gate_generic(const mcgmil::GateParams& gp, hipStream_t s) {
     std::call_once(once, [&] { raise_lds_cap(k); });
     const long long tiles = (gp.total_samples + BM - 1) / BM;
     if (tiles == 0) return MCGMIL_OK;
+    if (gp.uniform_rows <= 0)
+        if (int rc = launch_plan(gp, BM, s)) return rc;
     const size_t lds = mcgmil::gate_lds_bytes<E, BM, MAXC>(gp.L);
     hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(mcgmil::kGateThreads), lds, s, gp);
     hipError_t e = hipGetLastError();
@@ -131,6 +152,8 @@ int launch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
     std::call_once(once, [&] { raise_lds_cap(k); });
     const long long tiles = (gp.total_samples + mcgmil::kPipeBM - 1) / mcgmil::kPipeBM;
     if (tiles == 0) return MCGMIL_OK;
+    if (gp.uniform_rows <= 0)
+        if (int rc = launch_plan(gp, mcgmil::kPipeBM, s)) return rc;
     const size_t lds = mcgmil::pipe_lds_bytes<E, MAXC>();
     hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(mcgmil::kGateThreads), lds, s, gp);
     hipError_t e = hipGetLastError();
@@ -257,6 +280,8 @@ int mcgmil_gate_scores(const mcgmil_args* a, void* stream) {
     gp.logits = reinterpret_cast<float*>(static_cast<char*>(a->workspace) + l.logits_off);
     gp.zz = reinterpret_cast<float*>(static_cast<char*>(a->workspace) + l.zz_off);
     gp.stamps = static_cast<unsigned long long*>(a->debug);
+    gp.tile_bag = reinterpret_cast<const int32_t*>(static_cast<char*>(a->workspace) + l.plan_off);
+    gp.uniform_rows = a->uniform_bag_rows;
 
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (a->h_dtype == MCGMIL_BF16) return dispatch_gate<__bf16>(gp, a->L, a->h_dtype, s);

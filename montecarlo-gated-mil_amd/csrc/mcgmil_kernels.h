@@ -36,6 +36,8 @@ struct GateParams {
     uint32_t bag_base;
     int t_base;
     const uint32_t* bag_ids;       // per-bag Philox counters or nullptr (bag_base + b)
+    const int32_t* tile_bag;       // bag of each tile's first row (plan_tiles_kernel) or nullptr
+    int uniform_rows;              // N if every bag has N rows (arithmetic row map), else 0
     const uint8_t* keep_feat;      // replay masks (parity mode) or nullptr
     const uint8_t* keep_att;
     float* logits;                 // [T*total_rows, C]
@@ -65,15 +67,30 @@ constexpr int kRowInfo = 6;        // ints per row: hrow, t, n, bag, Nb, bag cou
 // Pieces shared by the two gate-score kernels.
 // ---------------------------------------------------------------------------------------
 
-// Row table of one BM-row tile of the flattened (bag, t, n) space (threads < BM).
+// Row table of one BM-row tile of the flattened (bag, t, n) space (threads < BM). With a tile
+// plan (bag of the tile's first row) a row walks forward over at most the few bags that start
+// inside the tile instead of binary-searching the CSR offsets (dependent L2 loads).
 template <int BM>
 __device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0, int* rinfo) {
     const int tid = threadIdx.x;
     if (tid >= BM) return;
     const long long R = R0 + tid;
     int hrow = -1, t = 0, n = 0, bag = 0, Nb = 0;
-    if (R < p.total_samples) {
-        bag = find_bag(p.bag_off, p.B, p.T, R);
+    if (R < p.total_samples && p.uniform_rows > 0) {
+        const long long per_bag = (long long)p.T * p.uniform_rows;
+        bag = (int)(R / per_bag);
+        Nb = p.uniform_rows;
+        const long long local = R - (long long)bag * per_bag;
+        t = (int)(local / Nb);
+        n = (int)(local - (long long)t * Nb);
+        hrow = bag * Nb + n;
+    } else if (R < p.total_samples) {
+        if (p.tile_bag) {
+            bag = p.tile_bag[blockIdx.x];
+            while ((long long)p.T * p.bag_off[bag + 1] <= R) ++bag;
+        } else {
+            bag = find_bag(p.bag_off, p.B, p.T, R);
+        }
         const int ob = p.bag_off[bag];
         Nb = p.bag_off[bag + 1] - ob;
         const long long local = R - (long long)p.T * ob;
@@ -84,6 +101,15 @@ __device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0
     int* ri = rinfo + kRowInfo * tid;
     ri[0] = hrow; ri[1] = t; ri[2] = n; ri[3] = bag; ri[4] = Nb;
     ri[5] = (int)(p.bag_ids ? p.bag_ids[bag] : p.bag_base + (uint32_t)bag);
+}
+
+// Tile plan: bag of the first row of every BM-row tile (one thread per tile).
+__global__ void plan_tiles_kernel(const int32_t* bag_off, int B, int T, long long total_samples,
+                                  int BM, long long tiles, int32_t* tile_bag) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= tiles) return;
+    const long long R = i * BM;
+    tile_bag[i] = R < total_samples ? find_bag(bag_off, B, T, R) : 0;
 }
 
 // tanh(x) * sigmoid(y) (reference model.py:183-184 / 287) evaluated as (1-a) / ((1+a)(1+b)),

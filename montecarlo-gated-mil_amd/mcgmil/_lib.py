@@ -32,7 +32,7 @@ class Args(ctypes.Structure):
         ("L", ctypes.c_int32), ("D", ctypes.c_int32), ("C", ctypes.c_int32),
         ("G", ctypes.c_int32), ("T", ctypes.c_int32), ("num_bags", ctypes.c_int32),
         ("total_rows", ctypes.c_int64),
-        ("h_dtype", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+        ("h_dtype", ctypes.c_int32), ("uniform_bag_rows", ctypes.c_int32),
         ("H", _vp), ("ldh", ctypes.c_int64), ("bag_offsets", _vp),
         ("Wv", _vp), ("bv", _vp), ("Wu", _vp), ("bu", _vp), ("wa", _vp), ("ba", _vp),
         ("wk", _vp), ("packed_w", _vp),

@@ -70,6 +70,12 @@ def _check_head(head: HeadTensors, device):
             raise ValueError(f"{name} is on {t.device}, H on {device}")
 
 
+class BagOffsets(torch.Tensor):
+    """int32 CSR offsets [B+1] on the device that remember, from the host-side sizes they were
+    built from, whether every bag has the same size (`uniform_rows`, 0 if ragged)."""
+    uniform_rows: int = 0
+
+
 def bag_offsets_tensor(sizes_or_offsets: Union[Sequence[int], torch.Tensor], device,
                        are_sizes: bool = True) -> torch.Tensor:
     """Build the int32 CSR offsets [B+1] on `device` from bag sizes (or offsets)."""
@@ -80,7 +86,11 @@ def bag_offsets_tensor(sizes_or_offsets: Union[Sequence[int], torch.Tensor], dev
         raise ValueError("bag offsets must start at 0 and be non-decreasing")
     if int(x[-1]) >= 2**31:
         raise ValueError("total rows must fit int32")
-    return x.to(device=device, dtype=torch.int32)
+    d = x[1:] - x[:-1]
+    uniform = int(d[0]) if bool((d == d[0]).all()) and int(d[0]) > 0 else 0
+    t = x.to(device=device, dtype=torch.int32).as_subclass(BagOffsets)
+    t.uniform_rows = uniform
+    return t
 
 
 def make_args(H: Optional[torch.Tensor], bag_offsets: torch.Tensor, head: Optional[HeadTensors],
@@ -104,6 +114,7 @@ def make_args(H: Optional[torch.Tensor], bag_offsets: torch.Tensor, head: Option
     else:
         a.ldh = a.L
     a.bag_offsets = _p(bag_offsets)
+    a.uniform_bag_rows = int(getattr(bag_offsets, "uniform_rows", 0))
     if head is not None:
         a.Wv, a.bv, a.Wu, a.bu = _p(head.Wv), _p(head.bv), _p(head.Wu), _p(head.bu)
         a.wa, a.ba, a.wk = _p(head.wa), _p(head.ba), _p(head.wk)
