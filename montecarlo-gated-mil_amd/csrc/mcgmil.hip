@@ -7,9 +7,10 @@
 #include <string>
 
 #include "../../include/mcgmil.h"
+#include "mcgmil_error.h"
 #include "mcgmil_kernels.h"
 
-namespace {
+namespace mcgmil_detail {
 
 thread_local std::string g_last_error;
 
@@ -21,6 +22,13 @@ int fail(int code, const std::string& msg) {
 int hip_fail(hipError_t e, const char* what) {
     return fail(MCGMIL_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
+
+}  // namespace mcgmil_detail
+
+namespace {
+
+using mcgmil_detail::fail;
+using mcgmil_detail::hip_fail;
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -196,7 +204,7 @@ int mcgmil_abi_version(void) { return MCGMIL_ABI_VERSION; }
 
 size_t mcgmil_args_size(void) { return sizeof(mcgmil_args); }
 
-const char* mcgmil_last_error(void) { return g_last_error.c_str(); }
+const char* mcgmil_last_error(void) { return mcgmil_detail::g_last_error.c_str(); }
 
 int mcgmil_packed_weights_size(const mcgmil_args* a, size_t* bytes) {
     int rc = validate_sizes(a);

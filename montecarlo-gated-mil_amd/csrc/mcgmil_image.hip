@@ -1,0 +1,677 @@
+// Image side of the path (include/mcgmil_image.h): the reference ImagePatcher's tile grid,
+// non-empty tile selection and bag gather (image_patcher.py:16-59,115-131), and the attention
+// maps with infer.py's mean/std over passes (image_patcher.py:62-110, infer.py:212-219).
+//
+// Everything is computed per *cell*: the union of all tile boundaries cuts the image into
+// disjoint rectangles, each lying wholly inside or outside every tile. One pass over channel 0
+// counts non-zero pixels per cell and adds the count to the (few) tiles covering the cell; the
+// attention maps are constant on each cell, so a map is T*C*cells values until the final
+// (write-bound) expansion to pixels. Byte/integer work, HBM-bound: no MFMA here.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/mcgmil_image.h"
+#include "mcgmil_device.h"
+#include "mcgmil_error.h"
+
+namespace {
+
+using mcgmil_detail::fail;
+using mcgmil_detail::hip_fail;
+using mcgmil::f32x4;
+using mcgmil::philox4x32_10;
+using mcgmil::wave_max;
+
+constexpr int kThreads = 256;
+constexpr int kMaxStarts = 4096;     // tile start points per dimension
+constexpr int kMaxCover = 4096;      // instances covering one cell (LDS list)
+constexpr uint32_t kShuffleTag = 0x5348464cu;   // "SHFL": Philox counter word of the shuffle
+
+// ---------------------------------------------------------------------------------------
+// Geometry, shared verbatim by host and device so both derive the same grid.
+// ---------------------------------------------------------------------------------------
+
+// image_patcher.py:16-28. The caller guarantees stride >= 1 and ps <= size.
+__host__ __device__ inline int start_points(int size, int ps, int stride, int32_t* out) {
+    int n = 0;
+    if (out) out[n] = 0;
+    ++n;
+    for (long long counter = 1;; ++counter) {
+        const long long pt = (long long)stride * counter;
+        if (pt + ps >= size) {
+            if (out) out[n] = size - ps;
+            ++n;
+            break;
+        }
+        if (out) out[n] = (int)pt;
+        ++n;
+    }
+    return n;
+}
+
+// Sorted union of {s[i]} and {s[i] + ps} (s non-decreasing): the cell boundaries of one axis.
+__host__ __device__ inline int merge_bounds(const int32_t* s, int n, int ps, int32_t* out) {
+    int i = 0, j = 0, m = 0, last = -1;
+    while (i < n || j < n) {
+        int v;
+        if (j >= n || (i < n && s[i] <= s[j] + ps)) v = s[i++];
+        else v = s[j++] + ps;
+        if (v != last) {
+            if (out) out[m] = v;
+            ++m;
+            last = v;
+        }
+    }
+    return m;
+}
+
+struct Geom {
+    int H, W, ps, stride;
+    int ny, nx;        // tile start points (rows, columns)
+    int nby, nbx;      // cell boundaries per axis (cells = boundaries - 1)
+    __host__ __device__ int cy() const { return nby - 1; }
+    __host__ __device__ int cx() const { return nbx - 1; }
+    __host__ __device__ long long cells() const { return (long long)cy() * cx(); }
+    __host__ __device__ long long tiles() const { return (long long)ny * nx; }
+};
+
+// Largest number of start points s with s <= p < s + ps over all positions p of one axis.
+int max_cover_1d(const std::vector<int32_t>& s, const std::vector<int32_t>& b, int ps) {
+    int best = 0;
+    for (size_t c = 0; c + 1 < b.size(); ++c) {
+        const int p = b[c];
+        const int hi = (int)(std::upper_bound(s.begin(), s.end(), p) - s.begin());
+        const int lo = (int)(std::upper_bound(s.begin(), s.end(), p - ps) - s.begin());
+        best = std::max(best, hi - lo);
+    }
+    return best;
+}
+
+int validate_geometry(const mcgmil_image_args* a, Geom* g, int* max_cover = nullptr) {
+    if (!a) return fail(MCGMIL_E_INVALID, "args is NULL");
+    if (a->height < 1 || a->width < 1) return fail(MCGMIL_E_INVALID, "image height/width must be >= 1");
+    if (a->patch_size < 1) return fail(MCGMIL_E_INVALID, "patch_size must be >= 1");
+    if (a->patch_size > a->height || a->patch_size > a->width)
+        return fail(MCGMIL_E_UNSUPPORTED, "patch_size larger than the image");
+    if (!(a->overlap >= 0.0 && a->overlap < 1.0)) return fail(MCGMIL_E_INVALID, "overlap must be in [0, 1)");
+    const int stride = (int)(a->patch_size * (1.0 - a->overlap));   // int(ps * (1 - overlap))
+    if (stride < 1) return fail(MCGMIL_E_INVALID, "stride int(patch_size * (1 - overlap)) is 0");
+    g->H = a->height;
+    g->W = a->width;
+    g->ps = a->patch_size;
+    g->stride = stride;
+    g->ny = start_points(g->H, g->ps, stride, nullptr);
+    g->nx = start_points(g->W, g->ps, stride, nullptr);
+    if (g->ny > kMaxStarts || g->nx > kMaxStarts)
+        return fail(MCGMIL_E_UNSUPPORTED, "more than 4096 tile start points per axis");
+    std::vector<int32_t> ys(g->ny), xs(g->nx);
+    start_points(g->H, g->ps, stride, ys.data());
+    start_points(g->W, g->ps, stride, xs.data());
+    g->nby = merge_bounds(ys.data(), g->ny, g->ps, nullptr);
+    g->nbx = merge_bounds(xs.data(), g->nx, g->ps, nullptr);
+    if (max_cover) {
+        std::vector<int32_t> yb(g->nby), xb(g->nbx);
+        merge_bounds(ys.data(), g->ny, g->ps, yb.data());
+        merge_bounds(xs.data(), g->nx, g->ps, xb.data());
+        *max_cover = max_cover_1d(ys, yb, g->ps) * max_cover_1d(xs, xb, g->ps);
+    }
+    return MCGMIL_OK;
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct Layout {
+    size_t ys, xs, yb, xb, rowcell, colcell, counts, sorted, cellval, cellstat, total;
+};
+
+Layout layout(const Geom& g, int T, int C) {
+    Layout l;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { const size_t at = o; o = align_up(o + bytes, 256); return at; };
+    l.ys = take(4 * (size_t)g.ny);
+    l.xs = take(4 * (size_t)g.nx);
+    l.yb = take(4 * (size_t)g.nby);
+    l.xb = take(4 * (size_t)g.nbx);
+    l.rowcell = take(4 * (size_t)g.H);
+    l.colcell = take(4 * (size_t)g.W);
+    l.counts = take(4 * (size_t)g.tiles());
+    l.sorted = take(4 * (size_t)g.tiles());
+    l.cellval = take(4 * (size_t)std::max(T, 0) * std::max(C, 0) * g.cells());
+    l.cellstat = take(8 * (size_t)std::max(C, 0) * g.cells());
+    l.total = o;
+    return l;
+}
+
+struct Ws {
+    int32_t *ys, *xs, *yb, *xb, *rowcell, *colcell, *counts, *sorted;
+    float *cellval, *cellstat;
+};
+
+Ws carve(void* base, const Layout& l) {
+    char* b = (char*)base;
+    return Ws{(int32_t*)(b + l.ys), (int32_t*)(b + l.xs), (int32_t*)(b + l.yb), (int32_t*)(b + l.xb),
+              (int32_t*)(b + l.rowcell), (int32_t*)(b + l.colcell), (int32_t*)(b + l.counts),
+              (int32_t*)(b + l.sorted), (float*)(b + l.cellval), (float*)(b + l.cellstat)};
+}
+
+// ---------------------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------------------
+
+// Grid setup. Blocks [0, by) map image rows to cells, blocks [by, by + bx) columns; each block
+// rebuilds its axis's starts and boundaries in LDS (a few hundred sequential steps) so no
+// block waits on another. Block 0 of each axis publishes the arrays; all blocks also zero the
+// tile counters.
+__global__ void __launch_bounds__(kThreads) grid_kernel(Geom g, int by, Ws w, int zero_counts) {
+    __shared__ int32_t s_starts[kMaxStarts];
+    __shared__ int32_t s_bounds[2 * kMaxStarts];
+    __shared__ int s_nb;
+    const bool rows = (int)blockIdx.x < by;
+    const int blk = rows ? blockIdx.x : blockIdx.x - by;
+    const int size = rows ? g.H : g.W;
+    if (threadIdx.x == 0) {
+        const int n = start_points(size, g.ps, g.stride, s_starts);
+        s_nb = merge_bounds(s_starts, n, g.ps, s_bounds);
+    }
+    __syncthreads();
+    const int n = rows ? g.ny : g.nx;
+    const int nb = s_nb;
+    if (blk == 0) {
+        int32_t* starts = rows ? w.ys : w.xs;
+        int32_t* bounds = rows ? w.yb : w.xb;
+        for (int i = threadIdx.x; i < n; i += kThreads) starts[i] = s_starts[i];
+        for (int i = threadIdx.x; i < nb; i += kThreads) bounds[i] = s_bounds[i];
+    }
+    const int p = blk * kThreads + threadIdx.x;
+    if (p < size) {   // cell = last boundary <= p (the final boundary == size is never <= p)
+        int lo = 0, hi = nb - 2;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_bounds[mid] <= p) lo = mid;
+            else hi = mid - 1;
+        }
+        (rows ? w.rowcell : w.colcell)[p] = lo;
+    }
+    if (zero_counts) {
+        const long long nt = g.tiles();
+        for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < nt;
+             i += (long long)gridDim.x * kThreads)
+            w.counts[i] = 0;
+    }
+}
+
+template <typename In> __device__ __forceinline__ float pixel(const In* p);
+template <> __device__ __forceinline__ float pixel<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float pixel<__bf16>(const __bf16* p) { return (float)*p; }
+template <> __device__ __forceinline__ float pixel<uint8_t>(const uint8_t* p) { return (float)*p; }
+template <> __device__ __forceinline__ float pixel<uint16_t>(const uint16_t* p) { return (float)*p; }
+
+// Non-zero pixels of channel 0 per cell (image_patcher.py:53 counts `> 0`), added to every
+// tile covering the cell. Integer atomics: the result is order-independent.
+template <typename In>
+__global__ void __launch_bounds__(kThreads) cell_count_kernel(Geom g, const In* img, long long ld_row,
+                                                              Ws w) {
+    const int cell = blockIdx.x;
+    const int cy = cell / g.cx(), cx = cell % g.cx();
+    const int y0 = w.yb[cy], y1 = w.yb[cy + 1], x0 = w.xb[cx], x1 = w.xb[cx + 1];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int cnt = 0;
+    for (int y = y0 + wave; y < y1; y += kThreads / 64) {
+        const In* row = img + (long long)y * ld_row;
+        for (int x = x0 + lane; x < x1; x += 64) cnt += pixel<In>(row + x) > 0.f;
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    __shared__ int s_cnt[kThreads / 64];
+    if (lane == 0) s_cnt[wave] = cnt;
+    __syncthreads();
+    const int total = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    if (total == 0) return;
+    // tile rows covering y0 x tile columns covering x0 (starts are non-decreasing)
+    for (int i = threadIdx.x; i < g.ny; i += kThreads) {
+        const int ty = w.ys[i];
+        if (!(ty <= y0 && y0 < ty + g.ps)) continue;
+        for (int j = 0; j < g.nx; ++j) {
+            const int tx = w.xs[j];
+            if (tx > x0) break;
+            if (x0 < tx + g.ps) atomicAdd(w.counts + (long long)i * g.nx + j, total);
+        }
+    }
+}
+
+__device__ __forceinline__ float nonzero_percent(int count, float area) {
+    return (float)count / area * 100.0f;   // == torch (mask.float().mean() * 100), fp32
+}
+
+// px, the kept count k and the stable rank order (px descending, tile index ascending):
+// tile i goes to position #{j : px_j > px_i or (px_j == px_i and j < i)} when that is < k.
+__global__ void __launch_bounds__(kThreads) select_kernel(Geom g, float thr, int cap, Ws w, float* px_out,
+                                                          int32_t* num_selected) {
+    __shared__ float s_px[kThreads];
+    const int nt = (int)g.tiles();
+    const float area = (float)(g.ps * g.ps);   // numel of a tile
+    const int i = blockIdx.x * kThreads + threadIdx.x;
+    const float pi = i < nt ? nonzero_percent(w.counts[i], area) : 0.f;
+    int rank = 0, above = 0;
+    for (int base = 0; base < nt; base += kThreads) {
+        __syncthreads();
+        const int j = base + threadIdx.x;
+        s_px[threadIdx.x] = j < nt ? nonzero_percent(w.counts[j], area) : -1.f;
+        __syncthreads();
+        const int m = min(kThreads, nt - base);
+        for (int jj = 0; jj < m; ++jj) {
+            const float pj = s_px[jj];
+            above += pj > thr;
+            rank += (pj > pi) || (pj == pi && base + jj < i);
+        }
+    }
+    const int k = min(above, cap);
+    if (i < nt) {
+        if (px_out) px_out[i] = pi;
+        if (rank < k) w.sorted[rank] = i;
+    }
+    if (i == 0) *num_selected = k;
+}
+
+// The bag order. shuffle: position of rank r = #{r' < k : key_r' < key_r or (== and r' < r)},
+// key_r = Philox4x32-10(counter {r, 0, 0, "SHFL"}, key = seed) word 0 -- a seeded permutation
+// standing in for sklearn.utils.shuffle (image_patcher.py:131).
+__global__ void __launch_bounds__(kThreads) order_kernel(Ws w, int shuffle, uint32_t k0, uint32_t k1,
+                                                         const int32_t* num_selected, int32_t* ids) {
+    __shared__ uint32_t s_key[kThreads];
+    const int k = *num_selected;
+    const int r = blockIdx.x * kThreads + threadIdx.x;
+    if (!shuffle) {
+        if (r < k) ids[r] = w.sorted[r];
+        return;
+    }
+    const uint32_t kr = philox4x32_10((uint32_t)r, 0u, 0u, kShuffleTag, k0, k1).x;
+    int pos = 0;
+    for (int base = 0; base < k; base += kThreads) {
+        __syncthreads();
+        s_key[threadIdx.x] = philox4x32_10((uint32_t)(base + threadIdx.x), 0u, 0u, kShuffleTag, k0, k1).x;
+        __syncthreads();
+        const int m = min(kThreads, k - base);
+        for (int jj = 0; jj < m; ++jj) {
+            const uint32_t kj = s_key[jj];
+            pos += (kj < kr) || (kj == kr && base + jj < r);
+        }
+    }
+    if (r < k) ids[pos] = w.sorted[r];
+}
+
+template <typename Out> __device__ __forceinline__ Out to_out(float v);
+template <> __device__ __forceinline__ float to_out<float>(float v) { return v; }
+template <> __device__ __forceinline__ __bf16 to_out<__bf16>(float v) { return (__bf16)v; }
+
+// instances[n, ch, r, :] = image[ch, y + r, x : x + ps] for n < k (image_patcher.py:52, the
+// float copy new_img[i] = image[...] then new_img[sorted_idx]). One wave per row.
+template <typename In, typename Out>
+__global__ void __launch_bounds__(kThreads) gather_kernel(Geom g, int channels, const In* img,
+                                                          long long ld_row, long long ld_ch, Ws w,
+                                                          const int32_t* ids, const int32_t* num_selected,
+                                                          Out* out) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long row = (long long)blockIdx.x * (kThreads / 64) + wave;   // over (n, ch, r)
+    const int ps = g.ps;
+    const long long n = row / ((long long)channels * ps);
+    if (n >= *num_selected) return;
+    const int rem = (int)(row - n * channels * ps);
+    const int ch = rem / ps, r = rem % ps;
+    const int t = ids[n];
+    const int ty = w.ys[t / g.nx], tx = w.xs[t % g.nx];
+    const In* src = img + ch * ld_ch + (long long)(ty + r) * ld_row + tx;
+    Out* dst = out + row * ps;
+    for (int x = lane; x < ps; x += 64) dst[x] = to_out<Out>(pixel<In>(src + x));
+}
+
+// Ordered list (instance order) of the instances whose tile covers the cell with top-left
+// (y0, x0), built in LDS chunk by chunk with ballot compaction. Returns the count.
+__device__ int collect_cover(const Geom& g, const Ws& w, const int32_t* ids, int k, int y0, int x0,
+                             int32_t* list, int* s_wave) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long nt = g.tiles();
+    int count = 0;
+    for (int base = 0; base < k; base += kThreads) {
+        const int item = base + threadIdx.x;
+        bool cov = false;
+        if (item < k) {
+            const int t = ids[item];
+            if (t >= 0 && t < nt) {
+                const int ty = w.ys[t / g.nx], tx = w.xs[t % g.nx];
+                cov = ty <= y0 && y0 < ty + g.ps && tx <= x0 && x0 < tx + g.ps;
+            }
+        }
+        const unsigned long long mask = __ballot(cov);
+        const int before = __popcll(mask & ((1ull << lane) - 1ull));
+        __syncthreads();                      // previous chunk's s_wave reads are done
+        if (lane == 0) s_wave[wave] = __popcll(mask);
+        __syncthreads();
+        int off = count;
+        for (int v = 0; v < wave; ++v) off += s_wave[v];
+        if (cov && off + before < kMaxCover) list[off + before] = item;
+        for (int v = 0; v < kThreads / 64; ++v) count += s_wave[v];
+    }
+    __syncthreads();
+    return count;
+}
+
+// Per (pass, class, cell): the covering instances' attention summed in instance order in fp32,
+// divided by the uint8 covering count (0 -> 1), as image_patcher.py:92-106 does per pixel.
+__global__ void __launch_bounds__(kThreads) cell_attention_kernel(Geom g, int TC, int k, const float* A,
+                                                                  const int32_t* ids, Ws w) {
+    __shared__ int32_t s_list[kMaxCover];
+    __shared__ int s_wave[kThreads / 64];
+    const long long cells = g.cells();
+    const int cell = blockIdx.x;
+    const int cy = cell / g.cx(), cx = cell % g.cx();
+    const int n = collect_cover(g, w, ids, k, w.yb[cy], w.xb[cx], s_list, s_wave);
+    const int c8 = n & 255;
+    const float div = (float)(c8 ? c8 : 1);
+    const int nl = min(n, kMaxCover);
+    for (int p = threadIdx.x; p < TC; p += kThreads) {
+        const float* a = A + (long long)p * k;
+        float acc = 0.f;
+        for (int q = 0; q < nl; ++q) acc += a[s_list[q]];
+        w.cellval[p * cells + cell] = acc / div;
+    }
+}
+
+// Per (pass, class): divide by the map's maximum (image_patcher.py:107-108). Every cell holds
+// at least one pixel, so the max over cells is the max over pixels.
+__global__ void __launch_bounds__(kThreads) normalize_kernel(Geom g, Ws w) {
+    __shared__ float s_max[kThreads / 64];
+    const long long cells = g.cells();
+    float* v = w.cellval + blockIdx.x * cells;
+    float m = -INFINITY;
+    for (long long i = threadIdx.x; i < cells; i += kThreads) m = fmaxf(m, v[i]);
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
+    for (long long i = threadIdx.x; i < cells; i += kThreads) v[i] = v[i] / m;
+}
+
+// Mean and unbiased std over the T passes per (class, cell), accumulated in fp64
+// (infer.py:216-219; torch's CPU reductions accumulate float in double).
+__global__ void __launch_bounds__(kThreads) cell_stats_kernel(Geom g, int T, int C, Ws w) {
+    const long long cells = g.cells();
+    const long long i = (long long)blockIdx.x * kThreads + threadIdx.x;   // over (c, cell)
+    if (i >= C * cells) return;
+    const int c = (int)(i / cells);
+    const long long cell = i % cells;
+    double s = 0.0;
+    for (int t = 0; t < T; ++t) s += (double)w.cellval[((long long)t * C + c) * cells + cell];
+    const double mean = s / T;
+    double q = 0.0;
+    for (int t = 0; t < T; ++t) {
+        const double d = (double)w.cellval[((long long)t * C + c) * cells + cell] - mean;
+        q += d * d;
+    }
+    w.cellstat[i] = (float)mean;
+    w.cellstat[C * cells + i] = T > 1 ? (float)sqrt(q / (T - 1)) : NAN;
+}
+
+// Expand per-cell planes to pixels: planes [0, P0) come from src0 into out0, planes [P0, P)
+// from src1 into out1 (each plane H x W). Nontemporal 16-byte stores when W % 4 == 0.
+__global__ void __launch_bounds__(kThreads) expand_kernel(Geom g, Ws w, int P0, const float* src0, float* out0,
+                                                          const float* src1, float* out1) {
+    const int y = blockIdx.x;
+    const int plane = blockIdx.y;
+    const long long cells = g.cells();
+    const bool first = plane < P0;
+    const float* src = first ? src0 + (long long)plane * cells : src1 + (long long)(plane - P0) * cells;
+    float* out = (first ? out0 + (long long)plane * g.H * g.W : out1 + (long long)(plane - P0) * g.H * g.W) +
+                 (long long)y * g.W;
+    const float* srow = src + (long long)w.rowcell[y] * g.cx();
+    if ((g.W & 3) == 0) {
+        const int4* cc = reinterpret_cast<const int4*>(w.colcell);
+        f32x4* o4 = reinterpret_cast<f32x4*>(out);
+        for (int x = threadIdx.x; x < g.W / 4; x += kThreads) {
+            const int4 c = cc[x];
+            f32x4 v = {srow[c.x], srow[c.y], srow[c.z], srow[c.w]};
+            __builtin_nontemporal_store(v, o4 + x);
+        }
+    } else {
+        for (int x = threadIdx.x; x < g.W; x += kThreads) __builtin_nontemporal_store(srow[w.colcell[x]], out + x);
+    }
+}
+
+// image_out[ch] = overlap average of the patches (image_patcher.py:62-80): per pixel the
+// covering patches summed in instance order in fp32, divided by the float count (0 -> 1).
+__global__ void __launch_bounds__(kThreads) reconstruct_kernel(Geom g, int channels, int k, const float* patches,
+                                                               const int32_t* ids, Ws w, float* out) {
+    __shared__ int32_t s_list[kMaxCover];
+    __shared__ int s_wave[kThreads / 64];
+    const int cell = blockIdx.x;
+    const int ch = blockIdx.y;
+    const int cy = cell / g.cx(), cx = cell % g.cx();
+    const int y0 = w.yb[cy], y1 = w.yb[cy + 1], x0 = w.xb[cx], x1 = w.xb[cx + 1];
+    const int n = collect_cover(g, w, ids, k, y0, x0, s_list, s_wave);
+    const float div = (float)(n ? n : 1);
+    const int nl = min(n, kMaxCover);
+    const int ps = g.ps;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int y = y0 + wave; y < y1; y += kThreads / 64) {
+        for (int x = x0 + lane; x < x1; x += 64) {
+            float acc = 0.f;
+            for (int q = 0; q < nl; ++q) {
+                const int item = s_list[q];
+                const int t = ids[item];
+                const int ty = w.ys[t / g.nx], tx = w.xs[t % g.nx];
+                acc += patches[(((long long)item * channels + ch) * ps + (y - ty)) * ps + (x - tx)];
+            }
+            out[((long long)ch * g.H + y) * g.W + x] = acc / div;
+        }
+    }
+}
+
+int check_launch(const char* what) {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, what);
+}
+
+int launch_grid(const Geom& g, const Ws& w, bool zero_counts, hipStream_t s) {
+    const int by = (g.H + kThreads - 1) / kThreads, bx = (g.W + kThreads - 1) / kThreads;
+    hipLaunchKernelGGL(grid_kernel, dim3(by + bx), dim3(kThreads), 0, s, g, by, w, zero_counts ? 1 : 0);
+    return check_launch("grid_kernel");
+}
+
+int check_workspace(const mcgmil_image_args* a, const Layout& l) {
+    if (!a->workspace) return fail(MCGMIL_E_WORKSPACE, "workspace is NULL");
+    if (((uintptr_t)a->workspace & 255u) != 0) return fail(MCGMIL_E_ALIGN, "workspace must be 256-byte aligned");
+    if (a->workspace_bytes < l.total)
+        return fail(MCGMIL_E_WORKSPACE, "workspace too small: need " + std::to_string(l.total) + " bytes");
+    return MCGMIL_OK;
+}
+
+template <typename In>
+int launch_count(const Geom& g, const mcgmil_image_args* a, const Ws& w, hipStream_t s) {
+    hipLaunchKernelGGL(cell_count_kernel<In>, dim3((unsigned)g.cells()), dim3(kThreads), 0, s, g,
+                       (const In*)a->image, (long long)a->ld_row, w);
+    return check_launch("cell_count_kernel");
+}
+
+template <typename In, typename Out>
+int launch_gather(const Geom& g, const mcgmil_image_args* a, const Ws& w, hipStream_t s) {
+    const long long rows = (long long)a->instance_capacity * a->channels * g.ps;
+    const long long blocks = (rows + kThreads / 64 - 1) / (kThreads / 64);
+    if (blocks == 0) return MCGMIL_OK;
+    hipLaunchKernelGGL((gather_kernel<In, Out>), dim3((unsigned)blocks), dim3(kThreads), 0, s, g, a->channels,
+                       (const In*)a->image, (long long)a->ld_row, (long long)a->ld_channel, w, a->tile_ids,
+                       a->num_selected, (Out*)a->instances);
+    return check_launch("gather_kernel");
+}
+
+template <typename In>
+int launch_gather_out(const Geom& g, const mcgmil_image_args* a, const Ws& w, hipStream_t s) {
+    return a->out_dtype == MCGMIL_BF16 ? launch_gather<In, __bf16>(g, a, w, s) : launch_gather<In, float>(g, a, w, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t mcgmil_image_args_size(void) { return sizeof(mcgmil_image_args); }
+
+int mcgmil_tile_grid(const mcgmil_image_args* a, int64_t* tiles, int32_t* n_tiles, int32_t* n_rows,
+                     int32_t* n_cols) {
+    Geom g;
+    int rc = validate_geometry(a, &g);
+    if (rc) return rc;
+    if (!n_tiles) return fail(MCGMIL_E_INVALID, "n_tiles is NULL");
+    *n_tiles = (int32_t)g.tiles();
+    if (n_rows) *n_rows = g.ny;
+    if (n_cols) *n_cols = g.nx;
+    if (tiles) {
+        std::vector<int32_t> ys(g.ny), xs(g.nx);
+        start_points(g.H, g.ps, g.stride, ys.data());
+        start_points(g.W, g.ps, g.stride, xs.data());
+        int64_t* t = tiles;
+        for (int i = 0; i < g.ny; ++i)
+            for (int j = 0; j < g.nx; ++j) {   // image_patcher.py:38 (y, x, ps, ps, i, j)
+                t[0] = ys[i]; t[1] = xs[j]; t[2] = g.ps; t[3] = g.ps; t[4] = i; t[5] = j;
+                t += 6;
+            }
+    }
+    return MCGMIL_OK;
+}
+
+int mcgmil_image_workspace_size(const mcgmil_image_args* a, size_t* bytes) {
+    Geom g;
+    int rc = validate_geometry(a, &g);
+    if (rc) return rc;
+    if (!bytes) return fail(MCGMIL_E_INVALID, "bytes is NULL");
+    *bytes = layout(g, a->T, a->C).total;
+    return MCGMIL_OK;
+}
+
+int mcgmil_image_to_bag(const mcgmil_image_args* a, void* stream) {
+    Geom g;
+    int rc = validate_geometry(a, &g);
+    if (rc) return rc;
+    if (a->bag_size != -1 && a->bag_size <= 0) return fail(MCGMIL_E_INVALID, "Invalid bag size");
+    if (a->channels < 1) return fail(MCGMIL_E_INVALID, "channels must be >= 1");
+    if (!a->image || !a->tile_ids || !a->num_selected)
+        return fail(MCGMIL_E_INVALID, "image, tile_ids and num_selected are required");
+    const int it = a->image_dtype;
+    if (it != MCGMIL_F32 && it != MCGMIL_BF16 && it != MCGMIL_U8 && it != MCGMIL_U16)
+        return fail(MCGMIL_E_INVALID, "image_dtype must be F32, BF16, U8 or U16");
+    if (a->ld_row < a->width || (a->channels > 1 && a->ld_channel < (int64_t)a->height * a->ld_row))
+        return fail(MCGMIL_E_INVALID, "image strides too small");
+    const long long nt = g.tiles();
+    if (nt > 0x7fffffffll) return fail(MCGMIL_E_UNSUPPORTED, "too many tiles");
+    const int cap = a->bag_size > 0 ? a->bag_size : 0x7fffffff;
+    if (a->instances) {
+        if (a->out_dtype != MCGMIL_F32 && a->out_dtype != MCGMIL_BF16)
+            return fail(MCGMIL_E_INVALID, "out_dtype must be F32 or BF16");
+        if ((long long)a->instance_capacity < std::min<long long>(nt, cap))
+            return fail(MCGMIL_E_INVALID, "instance_capacity < min(n_tiles, bag_size)");
+    }
+    const Layout l = layout(g, 0, 0);
+    if ((rc = check_workspace(a, l))) return rc;
+    const Ws w = carve(a->workspace, l);
+    hipStream_t s = (hipStream_t)stream;
+    if ((rc = launch_grid(g, w, true, s))) return rc;
+    switch (it) {
+        case MCGMIL_F32: rc = launch_count<float>(g, a, w, s); break;
+        case MCGMIL_BF16: rc = launch_count<__bf16>(g, a, w, s); break;
+        case MCGMIL_U8: rc = launch_count<uint8_t>(g, a, w, s); break;
+        default: rc = launch_count<uint16_t>(g, a, w, s); break;
+    }
+    if (rc) return rc;
+    const float thr = (float)(a->empty_thresh * 100.0);   // torch: fp32 tensor > python float
+    const unsigned tb = (unsigned)((nt + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(select_kernel, dim3(tb), dim3(kThreads), 0, s, g, thr, cap, w, a->px, a->num_selected);
+    if ((rc = check_launch("select_kernel"))) return rc;
+    hipLaunchKernelGGL(order_kernel, dim3(tb), dim3(kThreads), 0, s, w, a->shuffle ? 1 : 0,
+                       (uint32_t)a->shuffle_seed, (uint32_t)(a->shuffle_seed >> 32), a->num_selected, a->tile_ids);
+    if ((rc = check_launch("order_kernel"))) return rc;
+    if (!a->instances) return MCGMIL_OK;
+    switch (it) {
+        case MCGMIL_F32: return launch_gather_out<float>(g, a, w, s);
+        case MCGMIL_BF16: return launch_gather_out<__bf16>(g, a, w, s);
+        case MCGMIL_U8: return launch_gather_out<uint8_t>(g, a, w, s);
+        default: return launch_gather_out<uint16_t>(g, a, w, s);
+    }
+}
+
+int mcgmil_attention_maps(const mcgmil_image_args* a, void* stream) {
+    Geom g;
+    int max_cover = 0;
+    int rc = validate_geometry(a, &g, &max_cover);
+    if (rc) return rc;
+    if (a->T < 1 || a->C < 1 || a->k < 0) return fail(MCGMIL_E_INVALID, "need T >= 1, C >= 1, k >= 0");
+    if (a->k > 0 && (!a->attention || !a->map_tile_ids))
+        return fail(MCGMIL_E_INVALID, "attention and map_tile_ids are required");
+    if (!a->maps && !a->map_mean && !a->map_std) return fail(MCGMIL_E_INVALID, "no output requested");
+    if (max_cover > kMaxCover) return fail(MCGMIL_E_UNSUPPORTED, "more than 4096 tiles overlap one pixel");
+    if ((long long)a->T * a->C > 65535) return fail(MCGMIL_E_UNSUPPORTED, "T * C > 65535");
+    if (g.cells() > 0x7fffffffll) return fail(MCGMIL_E_UNSUPPORTED, "too many cells");
+    const Layout l = layout(g, a->T, a->C);
+    if ((rc = check_workspace(a, l))) return rc;
+    const Ws w = carve(a->workspace, l);
+    hipStream_t s = (hipStream_t)stream;
+    if ((rc = launch_grid(g, w, false, s))) return rc;
+    const int TC = a->T * a->C;
+    hipLaunchKernelGGL(cell_attention_kernel, dim3((unsigned)g.cells()), dim3(kThreads), 0, s, g, TC, a->k,
+                       a->attention, a->map_tile_ids, w);
+    if ((rc = check_launch("cell_attention_kernel"))) return rc;
+    hipLaunchKernelGGL(normalize_kernel, dim3(TC), dim3(kThreads), 0, s, g, w);
+    if ((rc = check_launch("normalize_kernel"))) return rc;
+    const bool stats = a->map_mean || a->map_std;
+    if (stats) {
+        const unsigned sb = (unsigned)((a->C * g.cells() + kThreads - 1) / kThreads);
+        hipLaunchKernelGGL(cell_stats_kernel, dim3(sb), dim3(kThreads), 0, s, g, a->T, a->C, w);
+        if ((rc = check_launch("cell_stats_kernel"))) return rc;
+    }
+    const long long plane = (long long)g.H * g.W;
+    // maps: T*C planes from cellval; statistics: C planes each, written where requested
+    if (a->maps) {
+        hipLaunchKernelGGL(expand_kernel, dim3(g.H, TC), dim3(kThreads), 0, s, g, w, TC, w.cellval, a->maps,
+                           w.cellval, a->maps);
+        if ((rc = check_launch("expand_kernel"))) return rc;
+    }
+    if (a->map_mean && a->map_std && a->map_std == a->map_mean + a->C * plane) {
+        hipLaunchKernelGGL(expand_kernel, dim3(g.H, 2 * a->C), dim3(kThreads), 0, s, g, w, 2 * a->C, w.cellstat,
+                           a->map_mean, w.cellstat, a->map_mean);
+        return check_launch("expand_kernel");
+    }
+    if (a->map_mean) {
+        hipLaunchKernelGGL(expand_kernel, dim3(g.H, a->C), dim3(kThreads), 0, s, g, w, a->C, w.cellstat,
+                           a->map_mean, w.cellstat, a->map_mean);
+        if ((rc = check_launch("expand_kernel"))) return rc;
+    }
+    if (a->map_std) {
+        const float* sd = w.cellstat + a->C * g.cells();
+        hipLaunchKernelGGL(expand_kernel, dim3(g.H, a->C), dim3(kThreads), 0, s, g, w, a->C, sd, a->map_std, sd,
+                           a->map_std);
+        if ((rc = check_launch("expand_kernel"))) return rc;
+    }
+    return MCGMIL_OK;
+}
+
+int mcgmil_reconstruct_image(const mcgmil_image_args* a, void* stream) {
+    Geom g;
+    int max_cover = 0;
+    int rc = validate_geometry(a, &g, &max_cover);
+    if (rc) return rc;
+    if (a->channels < 1 || a->k < 0) return fail(MCGMIL_E_INVALID, "need channels >= 1, k >= 0");
+    if (!a->image_out || (a->k > 0 && (!a->patches || !a->map_tile_ids)))
+        return fail(MCGMIL_E_INVALID, "patches, map_tile_ids and image_out are required");
+    if (max_cover > kMaxCover) return fail(MCGMIL_E_UNSUPPORTED, "more than 4096 tiles overlap one pixel");
+    if (a->channels > 65535) return fail(MCGMIL_E_UNSUPPORTED, "channels > 65535");
+    const Layout l = layout(g, 0, 0);
+    if ((rc = check_workspace(a, l))) return rc;
+    const Ws w = carve(a->workspace, l);
+    hipStream_t s = (hipStream_t)stream;
+    if ((rc = launch_grid(g, w, false, s))) return rc;
+    hipLaunchKernelGGL(reconstruct_kernel, dim3((unsigned)g.cells(), a->channels), dim3(kThreads), 0, s, g,
+                       a->channels, a->k, a->patches, a->map_tile_ids, w, a->image_out);
+    return check_launch("reconstruct_kernel");
+}
+
+}  // extern "C"

@@ -10,6 +10,8 @@ HIP kernels behind the C ABI in include/mcgmil.h (libmcgmil.so, loaded with ctyp
   infer.mc_predict_bags              caller-side uncertainty summary (reference infer.py)
   shard                              bag sharding + prediction gather across GPUs
   resnet                             in-repo ResNet backbone (torchvision is not available)
+  patcher.ImagePatcher               the reference ImagePatcher on the GPU (tiling, selection,
+                                     gather, attention maps + mean/std), include/mcgmil_image.h
 """
 from .model import MultiHeadGatedAttentionMIL, AuxiliaryLoss  # noqa: F401
 from .resnet import deactivate_batchnorm, Identity  # noqa: F401

@@ -11,8 +11,9 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(os.path.dirname(ROOT), "include")
 LIB = os.path.join(PKG, "libmcgmil.so")
-SOURCES = ["mcgmil.hip"]
-DEPS = ["mcgmil.hip", "mcgmil_kernels.h", "mcgmil_device.h"]
+SOURCES = ["mcgmil.hip", "mcgmil_image.hip"]
+DEPS = ["mcgmil.hip", "mcgmil_image.hip", "mcgmil_kernels.h", "mcgmil_device.h",
+        "mcgmil_error.h"]
 ARCH = os.environ.get("MCGMIL_OFFLOAD_ARCH", "gfx950")
 
 
@@ -20,7 +21,8 @@ def _stale(out: str = LIB) -> bool:
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
-    deps = [os.path.join(CSRC, d) for d in DEPS] + [os.path.join(INCLUDE, "mcgmil.h")]
+    deps = [os.path.join(CSRC, d) for d in DEPS] + \
+        [os.path.join(INCLUDE, h) for h in ("mcgmil.h", "mcgmil_image.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 

@@ -15,12 +15,17 @@ from . import _build
 
 MCGMIL_F32 = 0
 MCGMIL_BF16 = 1
+MCGMIL_U8 = 2
+MCGMIL_U16 = 3
 
 EXPORTED = (
     "mcgmil_abi_version", "mcgmil_args_size", "mcgmil_last_error", "mcgmil_workspace_size",
     "mcgmil_packed_weights_size", "mcgmil_pack_weights", "mcgmil_mcdo_forward",
     "mcgmil_gate_scores", "mcgmil_softmax_pool", "mcgmil_bag_stats", "mcgmil_feature_keep",
     "mcgmil_attention_keep",
+    # include/mcgmil_image.h
+    "mcgmil_image_args_size", "mcgmil_tile_grid", "mcgmil_image_workspace_size",
+    "mcgmil_image_to_bag", "mcgmil_attention_maps", "mcgmil_reconstruct_image",
 )
 
 _vp = ctypes.c_void_p
@@ -41,6 +46,24 @@ class Args(ctypes.Structure):
         ("keep_feat", _vp), ("keep_att", _vp),
         ("Y", _vp), ("A", _vp), ("A_mean", _vp), ("A_var", _vp), ("P_mean", _vp),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t), ("debug", _vp),
+    ]
+
+
+class ImageArgs(ctypes.Structure):
+    """Mirror of struct mcgmil_image_args (include/mcgmil_image.h)."""
+    _fields_ = [
+        ("height", ctypes.c_int32), ("width", ctypes.c_int32), ("channels", ctypes.c_int32),
+        ("patch_size", ctypes.c_int32), ("overlap", ctypes.c_double),
+        ("empty_thresh", ctypes.c_double), ("bag_size", ctypes.c_int32),
+        ("shuffle", ctypes.c_int32), ("shuffle_seed", ctypes.c_uint64),
+        ("image_dtype", ctypes.c_int32), ("out_dtype", ctypes.c_int32), ("image", _vp),
+        ("ld_row", ctypes.c_int64), ("ld_channel", ctypes.c_int64),
+        ("px", _vp), ("tile_ids", _vp), ("num_selected", _vp), ("instances", _vp),
+        ("instance_capacity", ctypes.c_int32),
+        ("T", ctypes.c_int32), ("C", ctypes.c_int32), ("k", ctypes.c_int32),
+        ("attention", _vp), ("map_tile_ids", _vp), ("maps", _vp), ("map_mean", _vp),
+        ("map_std", _vp), ("patches", _vp), ("image_out", _vp),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
     ]
 
 
@@ -84,6 +107,19 @@ def load():
         f = getattr(L, name)
         f.argtypes = [pa, _vp, _vp]
         f.restype = ctypes.c_int
+    pi = ctypes.POINTER(ImageArgs)
+    L.mcgmil_image_args_size.restype = ctypes.c_size_t
+    L.mcgmil_tile_grid.argtypes = [pi, _vp, _vp, _vp, _vp]
+    L.mcgmil_tile_grid.restype = ctypes.c_int
+    L.mcgmil_image_workspace_size.argtypes = [pi, ctypes.POINTER(ctypes.c_size_t)]
+    L.mcgmil_image_workspace_size.restype = ctypes.c_int
+    for name in ("mcgmil_image_to_bag", "mcgmil_attention_maps", "mcgmil_reconstruct_image"):
+        f = getattr(L, name)
+        f.argtypes = [pi, _vp]
+        f.restype = ctypes.c_int
+    if L.mcgmil_image_args_size() != ctypes.sizeof(ImageArgs):
+        raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_image_args)={L.mcgmil_image_args_size()} "
+                          f"but the ctypes mirror is {ctypes.sizeof(ImageArgs)} bytes")
     if L.mcgmil_args_size() != ctypes.sizeof(Args):
         raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_args)={L.mcgmil_args_size()} but the "
                           f"ctypes mirror is {ctypes.sizeof(Args)} bytes")

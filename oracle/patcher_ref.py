@@ -12,6 +12,7 @@ Only tests/ and bench.py's cpu_baseline leg may import this, as the checker.
                     order (percentage descending, tile index ascending) and no shuffle. The
                     SET of selected tiles is identical; the order differs only among ties, and
                     the MIL head is permutation-equivariant (tests/test_oracle_golden.py).
+  reconstruct_image image_patcher.py:62-80   (overlap-averaged patches, float counts)
   attention_maps    image_patcher.py:83-110  (overlap-averaged, per-(pass, class) max-normalised)
   map_stats         infer.py:212-219          mean / unbiased std over passes
 Pinned by tests/golden/patcher_*.npz (tests/golden/make_golden_patcher.py runs the reference).
@@ -69,6 +70,19 @@ def crops(image, tiles, ids):
     image = torch.as_tensor(image)
     return torch.stack([image[:, y:y + dh, x:x + dw] for (y, x, dh, dw, _, _) in tiles[ids]]) \
         if len(ids) else torch.zeros(0, image.shape[0], tiles[0][2], tiles[0][3])
+
+
+def reconstruct_image(patches, tiles, ids, image_shape):
+    patches = torch.as_tensor(patches)
+    c, h, w = image_shape
+    rec = torch.zeros(c, h, w, dtype=patches.dtype)
+    cnt = torch.zeros(c, h, w, dtype=torch.float32)
+    for item in range(len(ids)):
+        y, x, dh, dw, _, _ = tiles[ids[item]]
+        rec[:, y:y + dh, x:x + dw] += patches[item]
+        cnt[:, y:y + dh, x:x + dw] += 1
+    cnt = torch.where(cnt == 0, torch.ones_like(cnt), cnt)
+    return rec / cnt
 
 
 def attention_maps(A, tiles, ids, image_shape):

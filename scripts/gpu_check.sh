@@ -31,6 +31,8 @@ for s in $STEPS; do
         smoke) run smoke 420 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
         tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
         bench) run bench 600 python bench.py ;;
+        imgtests) run pytest_gpu_image 600 python -m pytest tests/test_gpu_image.py -m gpu -q -rf ;;
+        imgprobe) run probe_image 300 python scripts/probe_image.py ;;
         probe) run probe 300 python scripts/probe_gate.py ;;
         stamps) run stamps 300 python scripts/probe_stamps.py ;;
         ab) run ab 300 env MCGMIL_PROBE_LIBS="$(ls -1 /tmp/mcgmil_var/*.so 2>/dev/null | paste -sd, -)" \

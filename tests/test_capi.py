@@ -8,11 +8,11 @@ import pytest
 
 from conftest import REPO
 
-HEADER = os.path.join(REPO, "include", "mcgmil.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("mcgmil.h", "mcgmil_image.h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
+    src = "".join(open(h).read() for h in HEADERS)
     return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(mcgmil_\w+)\s*\(", src, re.M)))
 
 
@@ -44,6 +44,7 @@ def test_args_struct_matches_binding(hip_lib):
     from mcgmil import _lib
     assert hip_lib.mcgmil_abi_version() == 1
     assert hip_lib.mcgmil_args_size() == ctypes.sizeof(_lib.Args)
+    assert hip_lib.mcgmil_image_args_size() == ctypes.sizeof(_lib.ImageArgs)
 
 
 def _args(**kw):
