@@ -13,7 +13,9 @@ META = ("N", "T", "C", "L", "D", "shared", "p_f", "p_a", "h_seed", "w_seed", "ma
 
 
 def names(prefix=""):
-    return sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, prefix + "*.npz")))
+    """MCDO head golden cases (the patcher_* fixtures belong to tests/test_patcher_oracle.py)."""
+    return sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, prefix + "*.npz"))
+                  if not os.path.basename(f).startswith("patcher_"))
 
 
 class Case:
