@@ -87,9 +87,10 @@ def main():
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--shared", type=int, default=0)
-    ap.add_argument("--workload", choices=["cfg3", "cfg4"], default="cfg3",
+    ap.add_argument("--workload", choices=["cfg3", "cfg4", "cfg5"], default="cfg3",
                     help="cfg3: --bags bags of N=--n per GPU (weak scaling, the headline); "
-                         "cfg4: 4096 bags N~U(256,2048) LPT-sharded over the GPUs (strong scaling)")
+                         "cfg4: 4096 bags N~U(256,2048) LPT-sharded over the GPUs (strong scaling); "
+                         "cfg5: end-to-end image -> patcher -> ResNet-18 -> head -> maps (bench_cfg5.py)")
     ap.add_argument("--dist-backend", default="nccl", help=argparse.SUPPRESS)   # rehearsal: gloo
     ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)  # ranks on cuda:0
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -103,6 +104,15 @@ def main():
         dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", 0 if args.same_device else local)
     torch.cuda.set_device(dev)
+
+    if args.workload == "cfg5":
+        import bench_cfg5
+        out = bench_cfg5.run(args, world, rank, dev, PEAK_TFLOPS["bf16"])
+        if rank == 0:
+            print(json.dumps(out))
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from mcgmil import _lib, ops
     from oracle import synthetic  # seeded synthetic parameters only (not a compute path)

@@ -1,0 +1,153 @@
+"""BASELINE config 5 (bench.py --workload cfg5): end-to-end per-image MCDO inference on one
+MI355X per rank -- on-GPU ImagePatcher (7036 x 2800 synthetic mammogram, 3 channels, 224 px
+tiles, overlap 0.5, empty_thresh 0.5, the dataset's ImageNet Normalize fused) -> ResNet-18
+feature extractor (PyTorch-ROCm, bf16 autocast, batch-statistics BN over the bag) -> fused
+MCDO head kernel (T=100, separate attention, bf16 operands) -> softmax probabilities ->
+attention-map mean/std over passes on the image grid (infer.py:187-219 without the plotting).
+
+A step = one image through all of that, the image already resident in HBM. Each rank runs its
+own image per step (images are independent: weak scaling, no collective on the data path).
+`roofline` prices the dominant stage, the ResNet-18 convolutions (3.64 GFLOP per 224 x 224
+instance: 1.82 GMAC, torchvision's published count), against the bf16 dense MFMA peak.
+`cpu_baseline` times the same pipeline on the host (oracle/patcher_ref.py, the in-repo ResNet
+in fp32 and oracle/mcdo_ref.py with torch's dropout RNG) on a bounded sample, extrapolated to
+one image.
+"""
+import json
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+RESNET18_GFLOP = 3.64          # per 3 x 224 x 224 instance (2 x 1.82 GMAC)
+H_IMG, W_IMG, PS, OVERLAP, THRESH = 7036, 2800, 224, 0.5, 0.5
+
+
+def synthetic_mammogram(dev, seed=5):
+    """A breast-like positive region touching the left border on a zero background, grey
+    repeated to 3 channels as the dataset does (dataset.py: unsqueeze(0).repeat(3, 1, 1))."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    yy = torch.arange(H_IMG, device=dev, dtype=torch.float32)[:, None]
+    xx = torch.arange(W_IMG, device=dev, dtype=torch.float32)[None, :]
+    blob = 1 - ((yy - 0.5 * H_IMG) / (0.45 * H_IMG)) ** 2 - (xx / (0.85 * W_IMG)) ** 2
+    noise = torch.rand(H_IMG, W_IMG, device=dev, generator=g) * 0.05
+    img = torch.where(blob > 0, blob + noise, torch.zeros_like(blob))
+    return img[None].repeat(3, 1, 1).contiguous()
+
+
+def cpu_baseline(k, T, budget_s=20.0):
+    """The same pipeline on the host, bounded: the patcher on the whole image, the ResNet on a
+    sample of instances, the head and the maps on a few passes -- each scaled to one image."""
+    from mcgmil import MultiHeadGatedAttentionMIL, deactivate_batchnorm
+    from oracle import mcdo_ref, patcher_ref, synthetic
+    threads = torch.get_num_threads()
+    img = synthetic_mammogram(torch.device("cpu"))
+    t0 = time.perf_counter()
+    tiles = patcher_ref.tile_grid(H_IMG, W_IMG, PS, OVERLAP)
+    px = patcher_ref.nonzero_percent(img, tiles)
+    ids = patcher_ref.select(px, THRESH, -1)
+    t_patch = time.perf_counter() - t0
+    model = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=False)
+    model.apply(deactivate_batchnorm)
+    model.eval()
+    n_inst = 16
+    inst = patcher_ref.crops(img, tiles, ids[:n_inst])
+    with torch.no_grad():
+        model.extract_features(inst[:2][None])                           # warm-up
+        t0 = time.perf_counter()
+        model.extract_features(inst[None])
+        t_feat = (time.perf_counter() - t0) / n_inst * k
+    arrays = synthetic.head_arrays(synthetic.head_state_dict(0, C=2, shared=False), 2, False)
+    prm = mcdo_ref.HeadParams(arrays)
+    H = synthetic.bag_features(42, k, 512)
+    t_pass = 2
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        mcdo_ref.mc_inference_torch_rng(H, prm, t_pass, 0.1, 0.1)
+        t_head = (time.perf_counter() - t0) / t_pass * T
+    A = torch.softmax(torch.randn(t_pass, 1, 2, k), dim=-1)
+    t0 = time.perf_counter()
+    maps = patcher_ref.attention_maps(A, tiles, ids[:k], (1, H_IMG, W_IMG))
+    patcher_ref.map_stats(maps)
+    t_maps = (time.perf_counter() - t0) / t_pass * T
+    total = t_patch + t_feat + t_head + t_maps
+    return {"value": T / total, "unit": "bag-samples/s", "cores": threads, "kind": "port",
+            "sample": f"one 7036x2800 image extrapolated from: patcher on the whole image "
+                      f"({t_patch:.2f} s), ResNet-18 fp32 on {n_inst} of {k} instances "
+                      f"({t_feat:.1f} s scaled), MCDO head on {t_pass} of {T} passes "
+                      f"({t_head:.1f} s scaled), maps+stats on {t_pass} passes ({t_maps:.1f} s "
+                      f"scaled); torch {torch.__version__} CPU, {threads} threads"}
+
+
+def run(args, world, rank, dev, peak_tflops):
+    from mcgmil import MultiHeadGatedAttentionMIL, deactivate_batchnorm
+    from mcgmil.infer import mc_predict_image
+    from mcgmil.patcher import ImagePatcher
+    T = args.T
+    torch.manual_seed(0)
+    model = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=bool(args.shared))
+    model.apply(deactivate_batchnorm)                       # infer.py:154
+    model.compute_dtype = torch.bfloat16
+    model.to(dev).eval()
+    model.feature_extractor.to(memory_format=torch.channels_last)
+    patcher = ImagePatcher(patch_size=PS, overlap=OVERLAP, empty_thresh=THRESH)
+    patcher.get_tiles(H_IMG, W_IMG)
+    img = synthetic_mammogram(dev, seed=5 + rank)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(i, events=None):
+        return mc_predict_image(model, patcher, img, T=T, seed=1000 * rank + i, events=events)
+
+    for i in range(args.warmup):
+        out = step(i)
+    k = len(out["tiles_indices"])
+    stage_ms = {}
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evs = []
+    for i in range(args.steps):
+        ev = []
+        step(args.warmup + i, ev)
+        evs.append(ev)
+    stream.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    for ev in evs:
+        for (_, a), (name, b) in zip(ev[:-1], ev[1:]):
+            stage_ms[name] = stage_ms.get(name, 0.0) + a.elapsed_time(b) / args.steps
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0])
+    feat_tflops = k * RESNET18_GFLOP / stage_ms["features"]         # GFLOP / ms = TFLOP/s
+    if rank != 0:
+        return None
+    cpu = None if args.no_cpu_baseline else cpu_baseline(k, T)
+    images = world * args.steps
+    return {
+        "metric": "end-to-end images/sec x MCDO-samples (T=100), config 5", "value": images * T / el,
+        "unit": "bag-samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic 7036x2800 mammogram-like image, random-init ResNet-18 and head",
+        "config": {"workload": f"BASELINE config 5: {H_IMG}x{W_IMG} image -> {PS}px tiles "
+                               f"(overlap {OVERLAP}, {len(patcher.tiles)} tiles, k={k} kept) -> "
+                               f"ResNet-18 bf16 -> MCDO head T={T} -> attention map mean/std",
+                   "images_per_s": images / el, "instances_per_bag": k, "T": T,
+                   "stage_ms": stage_ms, "parallelism": f"one image per GPU per step, {world} GPU(s)"},
+        "roofline": {"bound": "mfma", "achieved": feat_tflops, "peak": peak_tflops, "unit": "TFLOP/s",
+                     "frac": feat_tflops / peak_tflops, "traffic": None,
+                     "kernel": "ResNet-18 feature extractor (MIOpen convolutions, the dominant stage)",
+                     "algorithmic_tflop_per_launch": k * RESNET18_GFLOP / 1e3},
+        "cpu_baseline": cpu,
+    }
+
+
+if __name__ == "__main__":
+    raise SystemExit("run through bench.py --workload cfg5")

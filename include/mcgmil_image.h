@@ -62,6 +62,9 @@ typedef struct mcgmil_image_args {
     /* ---- image (device), [c, H, W] with strides in elements ---- */
     int32_t image_dtype;        /* MCGMIL_F32, MCGMIL_BF16, MCGMIL_U8 or MCGMIL_U16 */
     int32_t out_dtype;          /* instances: MCGMIL_F32 or MCGMIL_BF16 */
+    int32_t normalize;          /* 1: instances = (x - norm_mean[ch]) / norm_std[ch] in fp32, the
+                                   dataset's T.Normalize (reference utils.py:50-51); c <= 4 */
+    float norm_mean[4], norm_std[4];
     const void* image;
     int64_t ld_row;             /* elements between rows (>= W) */
     int64_t ld_channel;         /* elements between channels (>= H * ld_row) */

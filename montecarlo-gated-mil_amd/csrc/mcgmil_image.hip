@@ -307,13 +307,22 @@ template <typename Out> __device__ __forceinline__ Out to_out(float v);
 template <> __device__ __forceinline__ float to_out<float>(float v) { return v; }
 template <> __device__ __forceinline__ __bf16 to_out<__bf16>(float v) { return (__bf16)v; }
 
+template <typename T, int N> using vec_t = T __attribute__((ext_vector_type(N)));
+
+struct Norm {
+    int on;
+    float mean[4], std[4];
+};
+
 // instances[n, ch, r, :] = image[ch, y + r, x : x + ps] for n < k (image_patcher.py:52, the
-// float copy new_img[i] = image[...] then new_img[sorted_idx]). One wave per row.
-template <typename In, typename Out>
+// float copy new_img[i] = image[...] then new_img[sorted_idx]), optionally normalised per
+// channel as the dataset's T.Normalize does: (x - mean) / std in fp32 (utils.py:50-51).
+// One wave per row, VEC elements per lane (VEC = 4 when rows and tiles are 4-aligned).
+template <typename In, typename Out, int VEC>
 __global__ void __launch_bounds__(kThreads) gather_kernel(Geom g, int channels, const In* img,
                                                           long long ld_row, long long ld_ch, Ws w,
                                                           const int32_t* ids, const int32_t* num_selected,
-                                                          Out* out) {
+                                                          Norm nm, Out* out) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const long long row = (long long)blockIdx.x * (kThreads / 64) + wave;   // over (n, ch, r)
     const int ps = g.ps;
@@ -325,7 +334,18 @@ __global__ void __launch_bounds__(kThreads) gather_kernel(Geom g, int channels, 
     const int ty = w.ys[t / g.nx], tx = w.xs[t % g.nx];
     const In* src = img + ch * ld_ch + (long long)(ty + r) * ld_row + tx;
     Out* dst = out + row * ps;
-    for (int x = lane; x < ps; x += 64) dst[x] = to_out<Out>(pixel<In>(src + x));
+    const float m = nm.on ? nm.mean[ch] : 0.f, sd = nm.on ? nm.std[ch] : 1.f;
+    for (int x = lane * VEC; x < ps; x += 64 * VEC) {
+        const vec_t<In, VEC> v = *reinterpret_cast<const vec_t<In, VEC>*>(src + x);
+        vec_t<Out, VEC> o;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+            float f = (float)v[e];
+            if (nm.on) f = (f - m) / sd;
+            o[e] = to_out<Out>(f);
+        }
+        *reinterpret_cast<vec_t<Out, VEC>*>(dst + x) = o;
+    }
 }
 
 // Ordered list (instance order) of the instances whose tile covers the cell with top-left
@@ -500,9 +520,25 @@ int launch_gather(const Geom& g, const mcgmil_image_args* a, const Ws& w, hipStr
     const long long rows = (long long)a->instance_capacity * a->channels * g.ps;
     const long long blocks = (rows + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks == 0) return MCGMIL_OK;
-    hipLaunchKernelGGL((gather_kernel<In, Out>), dim3((unsigned)blocks), dim3(kThreads), 0, s, g, a->channels,
-                       (const In*)a->image, (long long)a->ld_row, (long long)a->ld_channel, w, a->tile_ids,
-                       a->num_selected, (Out*)a->instances);
+    Norm nm;
+    nm.on = a->normalize ? 1 : 0;
+    for (int c = 0; c < 4; ++c) {
+        nm.mean[c] = a->norm_mean[c];
+        nm.std[c] = a->norm_std[c];
+    }
+    // 4-wide when every tile row starts 4-aligned: base, strides, tile starts and ps
+    const bool vec4 = ((uintptr_t)a->image % (4 * sizeof(In))) == 0 && a->ld_row % 4 == 0 &&
+                      (a->channels == 1 || a->ld_channel % 4 == 0) && g.ps % 4 == 0 && g.stride % 4 == 0 &&
+                      (g.W - g.ps) % 4 == 0 && ((uintptr_t)a->instances % 16) == 0;
+    const dim3 grid((unsigned)blocks), block(kThreads);
+    if (vec4)
+        hipLaunchKernelGGL((gather_kernel<In, Out, 4>), grid, block, 0, s, g, a->channels, (const In*)a->image,
+                           (long long)a->ld_row, (long long)a->ld_channel, w, a->tile_ids, a->num_selected, nm,
+                           (Out*)a->instances);
+    else
+        hipLaunchKernelGGL((gather_kernel<In, Out, 1>), grid, block, 0, s, g, a->channels, (const In*)a->image,
+                           (long long)a->ld_row, (long long)a->ld_channel, w, a->tile_ids, a->num_selected, nm,
+                           (Out*)a->instances);
     return check_launch("gather_kernel");
 }
 
@@ -566,6 +602,7 @@ int mcgmil_image_to_bag(const mcgmil_image_args* a, void* stream) {
     if (nt > 0x7fffffffll) return fail(MCGMIL_E_UNSUPPORTED, "too many tiles");
     const int cap = a->bag_size > 0 ? a->bag_size : 0x7fffffff;
     if (a->instances) {
+        if (a->normalize && a->channels > 4) return fail(MCGMIL_E_UNSUPPORTED, "normalize supports c <= 4");
         if (a->out_dtype != MCGMIL_F32 && a->out_dtype != MCGMIL_BF16)
             return fail(MCGMIL_E_INVALID, "out_dtype must be F32 or BF16");
         if ((long long)a->instance_capacity < std::min<long long>(nt, cap))

@@ -56,7 +56,9 @@ class ImageArgs(ctypes.Structure):
         ("patch_size", ctypes.c_int32), ("overlap", ctypes.c_double),
         ("empty_thresh", ctypes.c_double), ("bag_size", ctypes.c_int32),
         ("shuffle", ctypes.c_int32), ("shuffle_seed", ctypes.c_uint64),
-        ("image_dtype", ctypes.c_int32), ("out_dtype", ctypes.c_int32), ("image", _vp),
+        ("image_dtype", ctypes.c_int32), ("out_dtype", ctypes.c_int32),
+        ("normalize", ctypes.c_int32), ("norm_mean", ctypes.c_float * 4),
+        ("norm_std", ctypes.c_float * 4), ("image", _vp),
         ("ld_row", ctypes.c_int64), ("ld_channel", ctypes.c_int64),
         ("px", _vp), ("tile_ids", _vp), ("num_selected", _vp), ("instances", _vp),
         ("instance_capacity", ctypes.c_int32),

@@ -9,12 +9,21 @@ per bag, what the reference computes from (Y, A):
   mean entropy  -sum p log(p + 1e-10)                  infer.py:56-57
   attention mean / unbiased variance over passes       infer.py:216-219 (per instance; the
                                                        reference maps them onto the image)
+
+mc_predict_image is the whole per-image loop of infer.py:187-219 on one GPU (BASELINE config 5):
+image -> ImagePatcher bag (+ the dataset's T.Normalize, fused) -> ResNet feature extractor
+(PyTorch-ROCm, batch-statistics BN over the bag) -> MCDO head kernel -> softmax probabilities
+-> attention maps' mean/std over passes, reconstructed on the image grid.
 """
+import contextlib
 from typing import List, Optional, Sequence
 
 import torch
 
 from . import ops
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)   # reference utils.py:50-51 (val/test transforms)
+IMAGENET_STD = (0.229, 0.224, 0.225)
 
 
 def mc_predict_bags(model, bags: Sequence[torch.Tensor], T: int = 50, seed: Optional[int] = None,
@@ -54,3 +63,46 @@ def mc_predict_bags(model, bags: Sequence[torch.Tensor], T: int = 50, seed: Opti
             "A_mean": Am[b].view(C, n), "A_var": Av[b].view(C, n),
         })
     return res
+
+
+def _stage(events, name, stream):
+    if events is not None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        events.append((name, ev))
+
+
+@torch.no_grad()
+def mc_predict_image(model, patcher, image: torch.Tensor, T: int = 100, seed: Optional[int] = None,
+                     features_dtype: Optional[torch.dtype] = torch.bfloat16,
+                     normalize=(IMAGENET_MEAN, IMAGENET_STD), events: Optional[list] = None) -> dict:
+    """One image [c, H, W] on a HIP device (get_tiles(H, W) done) -> dict with the bag's tile
+    ids, its features [k, L], Y [T, C], A [T, C, k], probs [T, C], prob_mean [C],
+    per-instance A_mean/A_var [C, k], and the
+    attention maps' mean/std over passes att_mean/att_std [C, H, W] (infer.py:212-219).
+
+    features_dtype=bfloat16 runs the ResNet under autocast (bf16 convolutions, fp32 BN) on
+    bf16 instances; None keeps the reference's fp32. `events` (a list) collects per-stage HIP
+    events for timing."""
+    device = model._check_device(image.device)
+    stream = torch.cuda.current_stream(device)
+    if seed is None:
+        seed = int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
+    _stage(events, "start", stream)
+    inst_dtype = torch.float32 if features_dtype is None else features_dtype
+    inst, ids, _ = patcher.convert_img_to_bag(image, seed=seed, out_dtype=inst_dtype,
+                                              normalize=normalize)
+    _stage(events, "patcher", stream)
+    ctx = torch.autocast("cuda", dtype=features_dtype) if features_dtype is not None \
+        else contextlib.nullcontext()
+    with ctx:
+        H = model.extract_features(inst.contiguous(memory_format=torch.channels_last)[None])
+    _stage(events, "features", stream)
+    Y, A, st = model.mc_inference_features(H[0].float(), T=T, seed=seed, return_stats=True)
+    _stage(events, "mcdo_head", stream)
+    probs = torch.softmax(Y[:, 0], dim=-1)                      # infer.py:195
+    att_mean, att_std = patcher.attention_statistics(A, patcher.last_tile_ids, image.shape)
+    _stage(events, "attention_maps", stream)
+    return {"tiles_indices": ids, "features": H[0], "Y": Y[:, 0], "A": A[:, 0], "probs": probs,
+            "prob_mean": st["P_mean"][0], "A_mean": st["A_mean"][0], "A_var": st["A_var"][0],
+            "att_mean": att_mean, "att_std": att_std}

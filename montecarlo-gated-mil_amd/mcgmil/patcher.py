@@ -89,9 +89,14 @@ class ImagePatcher:
 
     # -- image -> bag --------------------------------------------------------------------
     def convert_img_to_bag(self, image: torch.Tensor, seed: Optional[int] = None,
-                           shuffle: bool = True, out_dtype: torch.dtype = torch.float32):
+                           shuffle: bool = True, out_dtype: torch.dtype = torch.float32,
+                           normalize: Optional[Tuple[Sequence[float], Sequence[float]]] = None):
         """image [c, H, W] on the HIP device -> (instances [k, c, ps, ps], instances_idx int64
-        [k], instances_cords int64 [k, 2]) like image_patcher.py:43-59. One host sync reads k."""
+        [k], instances_cords int64 [k, 2]) like image_patcher.py:43-59. One host sync reads k.
+
+        normalize=(mean, std) fuses the dataset's per-instance T.Normalize (reference
+        utils.py:50-51, applied in dataset.py:70-71) into the gather: (x - mean) / std in fp32,
+        bit-identical to torchvision's sub_/div_."""
         if not isinstance(image, torch.Tensor) or not image.is_cuda or image.dim() != 3:
             raise ValueError("image must be a [c, H, W] HIP tensor")
         if image.dtype not in _IMAGE_DTYPES:
@@ -112,6 +117,13 @@ class ImagePatcher:
         a.shuffle, a.shuffle_seed = int(bool(shuffle)), int(seed or 0) & (2 ** 64 - 1)
         a.image_dtype, a.out_dtype = _IMAGE_DTYPES[image.dtype], _OUT_DTYPES[out_dtype]
         a.image, a.ld_row, a.ld_channel = _p(image), image.stride(1), image.stride(0)
+        if normalize is not None:
+            mean, std = (np.asarray(v, dtype=np.float32).reshape(-1) for v in normalize)
+            if len(mean) != c or len(std) != c:
+                raise ValueError(f"normalize needs {c} means and stds")
+            a.normalize = 1
+            for i in range(c):
+                a.norm_mean[i], a.norm_std[i] = float(mean[i]), float(std[i])
         px = torch.empty(nt, dtype=torch.float32, device=dev)
         ids = torch.empty(nt, dtype=torch.int32, device=dev)
         count = torch.empty(1, dtype=torch.int32, device=dev)

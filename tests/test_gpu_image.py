@@ -101,6 +101,23 @@ def test_bf16_instances_and_strided_image(cuda):
     assert torch.equal(inst.cpu(), P.crops(img, z["tiles"], idx).to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("seed,out", [(11, torch.float32), (12, torch.bfloat16)])
+def test_fused_normalize(cuda, seed, out):
+    """dataset.py:70-71 applies T.Normalize(ImageNet mean/std) (utils.py:50-51) per instance;
+    torchvision computes tensor.sub_(mean).div_(std) with fp32 mean/std."""
+    z = _case(seed)
+    img = torch.from_numpy(synthetic_image(seed, int(z["h"]), int(z["w"]), 1)).repeat(3, 1, 1)
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    p = _patcher(z)
+    inst, idx, _ = p.convert_img_to_bag(img.to(cuda), shuffle=False, out_dtype=out,
+                                        normalize=(mean, std))
+    crops = P.crops(img, z["tiles"], idx)
+    m = torch.tensor(mean, dtype=torch.float32)[:, None, None]
+    s = torch.tensor(std, dtype=torch.float32)[:, None, None]
+    want = torch.stack([x.sub(m).div(s) for x in crops]).to(out)
+    assert torch.equal(inst.cpu(), want)
+
+
 def test_empty_and_capped_bags(cuda):
     from mcgmil.patcher import ImagePatcher
     p = ImagePatcher(patch_size=32, overlap=0.5, bag_size=-1, empty_thresh=0.5)

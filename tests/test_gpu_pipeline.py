@@ -1,0 +1,98 @@
+"""End-to-end per-image pipeline (mcgmil.infer.mc_predict_image, BASELINE config 5 shape at a
+small size): every stage checked against its CPU counterpart on the same inputs.
+
+  patcher    tile set = oracle selection; instances = normalised crops (bit-exact)
+  features   in-repo ResNet-18 on the GPU vs the same module on the CPU, fp32: rel <= 1e-3
+             (different convolution algorithms; BN over the bag's batch statistics)
+  head       the GPU's own features through the MCDO oracle with the kernel's Philox masks:
+             the fp32 bounds of tests/test_gpu_parity.py
+  maps       mean/std of the oracle's attention maps from the kernel's A: abs <= 1e-7"""
+import numpy as np
+import pytest
+import torch
+
+from golden.make_golden_patcher import synthetic_image
+from golden_util import nrel
+from oracle import mcdo_ref, patcher_ref as P, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _head_arrays(model):
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()
+          if not k.startswith("feature_extractor")}
+    return synthetic.head_arrays(sd, model.num_classes, model.shared_attention)
+
+
+@pytest.mark.parametrize("shared", [False, True])
+def test_mc_predict_image_stages(cuda, shared):
+    from mcgmil import MultiHeadGatedAttentionMIL, deactivate_batchnorm
+    from mcgmil.infer import IMAGENET_MEAN, IMAGENET_STD, mc_predict_image
+    from mcgmil.patcher import ImagePatcher
+    torch.manual_seed(0)
+    model = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=shared)
+    model.apply(deactivate_batchnorm)                                   # infer.py:154
+    model.to(cuda).eval()
+    h, w, ps, T, seed = 520, 400, 64, 12, 77
+    img = torch.from_numpy(synthetic_image(4, h, w, 1)).repeat(3, 1, 1)  # grey -> 3 channels
+    patcher = ImagePatcher(patch_size=ps, overlap=0.5, empty_thresh=0.6)
+    tiles = patcher.get_tiles(h, w)
+    ev = []
+    out = mc_predict_image(model, patcher, img.to(cuda), T=T, seed=seed, features_dtype=None,
+                           events=ev)
+    torch.cuda.synchronize()
+    assert [n for n, _ in ev] == ["start", "patcher", "features", "mcdo_head", "attention_maps"]
+    ids = out["tiles_indices"]
+    px = P.nonzero_percent(img, tiles)
+    assert sorted(ids.tolist()) == sorted(P.select(px, 0.6, -1).tolist())
+    k = len(ids)
+    assert k > 8
+
+    # features: the same ResNet on the CPU over the same normalised instances
+    m = torch.tensor(IMAGENET_MEAN)[:, None, None]
+    s = torch.tensor(IMAGENET_STD)[:, None, None]
+    inst = torch.stack([x.sub(m).div(s) for x in P.crops(img, tiles, ids)])
+    cpu_model = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=shared)
+    cpu_model.apply(deactivate_batchnorm)
+    cpu_model.load_state_dict({k_: v.cpu() for k_, v in model.state_dict().items()})
+    with torch.no_grad():
+        H_cpu = cpu_model.extract_features(inst[None])[0]
+    H_gpu = out["features"].float()
+    assert nrel(H_gpu.cpu().numpy(), H_cpu.numpy()) <= 1e-3
+
+    # head: the kernel's outputs from the GPU features equal the oracle's on those features
+    arrays = _head_arrays(model)
+    kF, kA = mcdo_ref.masks_for_bag(seed, 0, T, k, 512, 2, 0.1, 0.1)
+    Y, A = mcdo_ref.mc_inference(H_gpu.cpu().numpy(), mcdo_ref.HeadParams(arrays), kF, kA, 0.1, 0.1)
+    assert np.abs(out["Y"].cpu().numpy() - Y[:, 0]).max() <= 1e-5
+    A_t = A[:, 0]                                                       # [T, C, k]
+    assert nrel(out["A_mean"].cpu().numpy(), A_t.mean(0)) <= 1e-5
+    probs = torch.softmax(torch.from_numpy(Y[:, 0]), dim=-1)
+    assert torch.allclose(out["probs"].cpu(), probs, atol=1e-5)
+
+    assert nrel(out["A"].cpu().numpy(), A_t) <= 1e-5
+
+    # maps: oracle maps of the kernel's attention (instances in the bag's shuffled order)
+    maps = P.attention_maps(out["A"].cpu()[:, None], tiles, ids, (1, h, w))
+    mean, std = P.map_stats(maps)
+    torch.testing.assert_close(out["att_mean"].cpu(), mean, rtol=0, atol=1e-7)
+    torch.testing.assert_close(out["att_std"].cpu(), std, rtol=0, atol=1e-7)
+
+
+def test_mc_predict_image_bf16_features(cuda):
+    """bf16 instances + autocast ResNet: predictions close to the fp32 pipeline."""
+    from mcgmil import MultiHeadGatedAttentionMIL, deactivate_batchnorm
+    from mcgmil.infer import mc_predict_image
+    from mcgmil.patcher import ImagePatcher
+    torch.manual_seed(1)
+    model = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=False)
+    model.apply(deactivate_batchnorm)
+    model.to(cuda).eval()
+    img = torch.from_numpy(synthetic_image(6, 448, 336, 1)).repeat(3, 1, 1).to(cuda)
+    patcher = ImagePatcher(patch_size=64, overlap=0.5, empty_thresh=0.5)
+    patcher.get_tiles(448, 336)
+    a = mc_predict_image(model, patcher, img, T=20, seed=3, features_dtype=None)
+    b = mc_predict_image(model, patcher, img, T=20, seed=3, features_dtype=torch.bfloat16)
+    assert np.array_equal(a["tiles_indices"], b["tiles_indices"])
+    assert (a["prob_mean"] - b["prob_mean"]).abs().max() < 2e-2
+    assert torch.isfinite(b["att_mean"]).all() and torch.isfinite(b["att_std"]).all()
