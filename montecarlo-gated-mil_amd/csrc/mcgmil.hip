@@ -269,6 +269,7 @@ int mcgmil_gate_scores(const mcgmil_args* a, void* stream) {
     gp.P = a->G * (a->D / 16);
     gp.total_samples = (long long)a->T * a->total_rows;
     gp.Wp = packed_ptr(a);
+    gp.wp_bytes = (uint32_t)packed_bytes_for(a);
     gp.bv = a->bv;
     gp.bu = a->bu;
     gp.wa = a->wa;

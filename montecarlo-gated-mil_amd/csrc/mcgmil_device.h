@@ -14,16 +14,24 @@ constexpr int kWave = 64;
 // Philox4x32-10 (Salmon et al. SC'11). Bit-exact with oracle/philox_oracle.c; the key words
 // are wave-uniform (the seed), so the key schedule lives in SGPRs.
 // ---------------------------------------------------------------------------------------
+// FLIP_XZ: output words x and z come out XORed with 0x80008000 (the sign flip of the packed
+// keep rule, drop_mask16x2_flipped) -- folded into the last round's key words, i.e. free.
+template <bool FLIP_XZ = false>
 __device__ __forceinline__ uint4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
+        if (FLIP_XZ && r == 9) {
+            k0 ^= 0x80008000u;
+            k1 ^= 0x80008000u;
+        }
         // one v_mad_u64_u32 per product gives both halves (measured: the cost of one
         // v_mul_hi_u32, half of a separate mul_lo + mul_hi pair)
         const uint64_t p0 = (uint64_t)c0 * 0xD2511F53u;
         const uint64_t p1 = (uint64_t)c2 * 0xCD9E8D57u;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        // hi ^ c ^ key as ONE v_bitop3_b32 (truth table 0x96; gfx950 has no v_xor3_b32)
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
         c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
@@ -39,6 +47,13 @@ __device__ __forceinline__ uint4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t drop_mask16x2(uint32_t word, uint32_t thrx) {
     const s16x2 u = __builtin_bit_cast(s16x2, word ^ 0x80008000u);
+    const s16x2 d = __builtin_elementwise_sub_sat(u, __builtin_bit_cast(s16x2, thrx));
+    return __builtin_bit_cast(uint32_t, d >> (s16x2){15, 15});
+}
+
+// drop_mask16x2 of a word that is already XORed with 0x80008000.
+__device__ __forceinline__ uint32_t drop_mask16x2_flipped(uint32_t flipped, uint32_t thrx) {
+    const s16x2 u = __builtin_bit_cast(s16x2, flipped);
     const s16x2 d = __builtin_elementwise_sub_sat(u, __builtin_bit_cast(s16x2, thrx));
     return __builtin_bit_cast(uint32_t, d >> (s16x2){15, 15});
 }
@@ -94,6 +109,30 @@ __device__ __forceinline__ Frag<float> load_frag(const float* p) {
     f.hi = *reinterpret_cast<const f32x4*>(p + 4);
     return f;
 }
+// Fragment loads through a buffer descriptor: voffset = the lane's byte offset, soffset = a
+// wave-uniform byte offset (SGPR), so address arithmetic stays scalar. DATA_FORMAT=32 in
+// word 3 (0x00020000), stride 0, range = bytes.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+template <typename E>
+__device__ __forceinline__ Frag<E> load_frag_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff);
+template <>
+__device__ __forceinline__ Frag<__bf16> load_frag_buf<__bf16>(__amdgpu_buffer_rsrc_t r, uint32_t voff,
+                                                              uint32_t soff) {
+    Frag<__bf16> f;
+    f.v = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+    return f;
+}
+template <>
+__device__ __forceinline__ Frag<float> load_frag_buf<float>(__amdgpu_buffer_rsrc_t r, uint32_t voff,
+                                                            uint32_t soff) {
+    Frag<float> f;
+    f.lo = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+    f.hi = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16u, soff, 0));
+    return f;
+}
+
 template <typename E> __device__ __forceinline__ Frag<E> zero_frag();
 template <> __device__ __forceinline__ Frag<__bf16> zero_frag<__bf16>() {
     Frag<__bf16> f; f.v = bf16x8{}; return f;

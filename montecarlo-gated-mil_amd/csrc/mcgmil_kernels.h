@@ -25,6 +25,7 @@ struct GateParams {
     int B, T, L, D, C, G, P;       // P = G * D / 16 gate tile pairs
     long long total_samples;       // T * total_rows
     const void* Wp;                // packed weights (see pack_weights_kernel)
+    uint32_t wp_bytes;             // their size (buffer-descriptor range)
     const float* bv;
     const float* bu;
     const float* wa;
@@ -283,21 +284,23 @@ __device__ __forceinline__ void store_masked(const Raw<float>& h, uint32_t kb, f
 }
 
 // Stage 8 features with the keep rule applied straight to the Philox words (2 draws each).
+// `o` comes from philox4x32_10<true>: words x and z are already sign-flipped.
 __device__ __forceinline__ void store_dropped(const Raw<__bf16>& h, uint4 o, uint32_t thrx,
                                               uint32_t inval, __bf16* dst) {
+    // v & ~(drop | inval) as one v_bitop3_b32 (truth table 0x10: a & ~b & ~c)
     uint4 v = h.v;
-    v.x &= ~(drop_mask16x2(o.x, thrx) | inval);
-    v.y &= ~(drop_mask16x2(o.y, thrx) | inval);
-    v.z &= ~(drop_mask16x2(o.z, thrx) | inval);
-    v.w &= ~(drop_mask16x2(o.w, thrx) | inval);
+    v.x = __builtin_amdgcn_bitop3_b32(v.x, drop_mask16x2_flipped(o.x, thrx), inval, 0x10);
+    v.y = __builtin_amdgcn_bitop3_b32(v.y, drop_mask16x2(o.y, thrx), inval, 0x10);
+    v.z = __builtin_amdgcn_bitop3_b32(v.z, drop_mask16x2_flipped(o.z, thrx), inval, 0x10);
+    v.w = __builtin_amdgcn_bitop3_b32(v.w, drop_mask16x2(o.w, thrx), inval, 0x10);
     *reinterpret_cast<uint4*>(dst) = v;
 }
 __device__ __forceinline__ uint32_t keep_lo(uint32_t m) { return ~(uint32_t)((int32_t)(m << 16) >> 16); }
 __device__ __forceinline__ uint32_t keep_hi(uint32_t m) { return ~(uint32_t)((int32_t)m >> 16); }
 __device__ __forceinline__ void store_dropped(const Raw<float>& h, uint4 o, uint32_t thrx,
                                               uint32_t inval, float* dst) {
-    const uint32_t m0 = drop_mask16x2(o.x, thrx) | inval, m1 = drop_mask16x2(o.y, thrx) | inval;
-    const uint32_t m2 = drop_mask16x2(o.z, thrx) | inval, m3 = drop_mask16x2(o.w, thrx) | inval;
+    const uint32_t m0 = drop_mask16x2_flipped(o.x, thrx) | inval, m1 = drop_mask16x2(o.y, thrx) | inval;
+    const uint32_t m2 = drop_mask16x2_flipped(o.z, thrx) | inval, m3 = drop_mask16x2(o.w, thrx) | inval;
     f32x4 a = h.lo, b = h.hi;
     a.x = __uint_as_float(__float_as_uint(a.x) & keep_lo(m0));
     a.y = __uint_as_float(__float_as_uint(a.y) & keep_hi(m0));
@@ -321,10 +324,6 @@ constexpr int VPM = MCGMIL_VPM;   // VALU instructions scheduled after each MFMA
 #endif
 #ifndef MCGMIL_SCHED
 #define MCGMIL_SCHED 0
-#endif
-#ifndef MCGMIL_ATT_IN_LOOP
-#define MCGMIL_ATT_IN_LOOP 0        // 1: draw the attention-logit keep in the K loop's last
-                                    // step (measured slower: 790 vs 825 TFLOP/s)
 #endif
 
 template <typename E, int MAXC>
@@ -368,39 +367,38 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
                                 : nullptr;
 
     const uint32_t inval = valid ? 0u : 0xFFFFFFFFu;   // padding rows stage zeros
-    // The staging of step KS is never read (idle slot); its Philox call draws this thread's
-    // attention-logit keep instead: (row, class kq), counter {n>>3, c, t | 2^31, bag}.
-    bool akeep = true;
     auto stage = [&](int s, const Raw<E>& h, E* slot) {
         if constexpr (REPLAY) {
             const uint32_t kb = kfe[(size_t)(s < KS ? s : KS - 1) * 4];  // step KS: dummy, in-row
             store_masked(h, kb & ~inval, slot + tid * 8);
-        } else {
-            const bool att = MCGMIL_ATT_IN_LOOP && s == KS;
+        } else {   // (the staging of step KS lands in the idle slot and is never read)
 #if MCGMIL_DIAG & 4   // ablation: no Philox (keep pattern from the counters)
             const uint4 o = make_uint4(cn * 0x9E3779B9u + (uint32_t)s, ct ^ cb, cn + ct, (uint32_t)s * 77u);
 #else
-            const uint4 o = philox4x32_10(att ? (cn >> 3) : (uint32_t)(s * 4 + kq),
-                                          att ? (uint32_t)kq : cn,
-                                          att ? (ct | 0x80000000u) : ct, cb, p.k0, p.k1);
+            const uint4 o = philox4x32_10<true>((uint32_t)(s * 4 + kq), cn, ct, cb, p.k0, p.k1);
 #endif
             store_dropped(h, o, p.thrx_f, inval, slot + tid * 8);
-            akeep = att ? draw_u16(o, (int)(cn & 7u)) >= p.thr_a : akeep;
         }
     };
 
-    // weight tiles of this wave (idle pair slots read a valid tile; fold_pairs skips them)
-    const E* Wp = reinterpret_cast<const E*>(p.Wp);
-    const size_t tile_elems = (size_t)KS * 512;
-    const int q0 = wave * PPW;
-    const E* wbase[NJ];
+    // weight tiles of this wave (idle pair slots read a valid tile; fold_pairs skips them).
+    // Buffer loads: one descriptor over the packed weights, the lane's byte offset as voffset
+    // and the wave-uniform tile + step offset as soffset, so the per-step address arithmetic
+    // is SALU only (no 64-bit VALU pointer increments in the K loop).
+    const __amdgpu_buffer_rsrc_t wrs = make_rsrc(p.Wp, p.wp_bytes);
+    const uint32_t tile_bytes = (uint32_t)KS * 512u * (uint32_t)sizeof(E);
+    constexpr uint32_t kStepBytes = 512u * (uint32_t)sizeof(E);
+    const int q0 = __builtin_amdgcn_readfirstlane(wave) * PPW;
+    uint32_t wsoff[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         int q = q0 + (j >> 1);
         q = q < p.P ? q : p.P - 1;
-        wbase[j] = Wp + (size_t)(2 * q + (j & 1)) * tile_elems + lane * 8;
+        wsoff[j] = (uint32_t)(2 * q + (j & 1)) * tile_bytes;
     }
-    const E* zbase = Wp + (size_t)(2 * p.P) * tile_elems + lane * 8;
+    const uint32_t zsoff = (uint32_t)(2 * p.P) * tile_bytes;
+    const uint32_t lane_b = (uint32_t)lane * 8u * (uint32_t)sizeof(E);
+    auto wfrag = [&](uint32_t soff) { return load_frag_buf<E>(wrs, lane_b, soff); };
 
     f32x4 acc[RT][NJ];
 #pragma unroll
@@ -429,8 +427,8 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
         zn = z;
 #else
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) wn[j] = load_frag(wbase[j] + (size_t)s1 * 512);
-        zn = load_frag(zbase + (size_t)s1 * 512);
+        for (int j = 0; j < NJ; ++j) wn[j] = wfrag(wsoff[j] + (uint32_t)s1 * kStepBytes);
+        zn = wfrag(zsoff + (uint32_t)s1 * kStepBytes);
 #endif
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
@@ -478,8 +476,8 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     stage(0, hA, Xs);
     hB = load_raw(hsrc + 32);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) wA[j] = load_frag(wbase[j]);
-    zA = load_frag(zbase);
+    for (int j = 0; j < NJ; ++j) wA[j] = wfrag(wsoff[j]);
+    zA = wfrag(zsoff);
     __syncthreads();
     MCGMIL_STAMP(p, 2);
 
@@ -499,7 +497,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     // ONE_CLASS: the wave's pairs all belong to gate q0 / (D/16) (idle waves: class >= C)
     const int one_class = ONE_CLASS ? (q0 < p.P ? q0 / (p.D >> 4) : MAXC) : -1;
     finish_scores<BM, MAXC>(p, R0, part, zacc, true, red, zred, rinfo, one_class,
-                            ONE_CLASS ? (p.D >> 4) / PPW : 0, !REPLAY && MCGMIL_ATT_IN_LOOP, akeep);
+                            ONE_CLASS ? (p.D >> 4) / PPW : 0, false, true);
     MCGMIL_STAMP(p, 7);
 }
 

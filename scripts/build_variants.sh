@@ -7,7 +7,8 @@ rm -f /tmp/mcgmil_var/*.so
 for spec in "$@"; do
     name=${spec%%:*}; defs=${spec#*:}
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -Iinclude $defs \
-        -o /tmp/mcgmil_var/$name.so montecarlo-gated-mil_amd/csrc/mcgmil.hip &
+        -o /tmp/mcgmil_var/$name.so montecarlo-gated-mil_amd/csrc/mcgmil.hip \
+        montecarlo-gated-mil_amd/csrc/mcgmil_image.hip &
 done
 wait
 ls /tmp/mcgmil_var

@@ -6,7 +6,7 @@ small size): every stage checked against its CPU counterpart on the same inputs.
              (different convolution algorithms; BN over the bag's batch statistics)
   head       the GPU's own features through the MCDO oracle with the kernel's Philox masks:
              the fp32 bounds of tests/test_gpu_parity.py
-  maps       mean/std of the oracle's attention maps from the kernel's A: abs <= 1e-7"""
+  maps       mean/std of the oracle's attention maps from the kernel's A: abs <= 2.4e-7"""
 import numpy as np
 import pytest
 import torch
@@ -16,6 +16,10 @@ from golden_util import nrel
 from oracle import mcdo_ref, patcher_ref as P, synthetic
 
 pytestmark = pytest.mark.gpu
+
+# mean/std over passes: fp64 accumulation here, torch's float reductions in the reference --
+# the results may differ in the last place; maps are <= 1, so 2 ulp of 1.0
+STAT_ATOL = 2.4e-7
 
 
 def _head_arrays(model):
@@ -64,6 +68,7 @@ def test_mc_predict_image_stages(cuda, shared):
     arrays = _head_arrays(model)
     kF, kA = mcdo_ref.masks_for_bag(seed, 0, T, k, 512, 2, 0.1, 0.1)
     Y, A = mcdo_ref.mc_inference(H_gpu.cpu().numpy(), mcdo_ref.HeadParams(arrays), kF, kA, 0.1, 0.1)
+    Y, A = np.asarray(Y), np.asarray(A)
     assert np.abs(out["Y"].cpu().numpy() - Y[:, 0]).max() <= 1e-5
     A_t = A[:, 0]                                                       # [T, C, k]
     assert nrel(out["A_mean"].cpu().numpy(), A_t.mean(0)) <= 1e-5
@@ -75,8 +80,8 @@ def test_mc_predict_image_stages(cuda, shared):
     # maps: oracle maps of the kernel's attention (instances in the bag's shuffled order)
     maps = P.attention_maps(out["A"].cpu()[:, None], tiles, ids, (1, h, w))
     mean, std = P.map_stats(maps)
-    torch.testing.assert_close(out["att_mean"].cpu(), mean, rtol=0, atol=1e-7)
-    torch.testing.assert_close(out["att_std"].cpu(), std, rtol=0, atol=1e-7)
+    torch.testing.assert_close(out["att_mean"].cpu(), mean, rtol=0, atol=STAT_ATOL)
+    torch.testing.assert_close(out["att_std"].cpu(), std, rtol=0, atol=STAT_ATOL)
 
 
 def test_mc_predict_image_bf16_features(cuda):
