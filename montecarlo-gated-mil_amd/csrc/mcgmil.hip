@@ -1,6 +1,7 @@
 // C ABI (include/mcgmil.h) over the gfx950 MCDO kernels: validation, workspace layout,
 // kernel selection and stream-ordered launches. No allocation, no host synchronisation.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -9,6 +10,7 @@
 #include "../../include/mcgmil.h"
 #include "mcgmil_error.h"
 #include "mcgmil_kernels.h"
+#include "mcgmil_gate_pp.h"
 
 namespace mcgmil_detail {
 
@@ -168,6 +170,44 @@ int launch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_pipe_kernel launch");
 }
 
+template <typename E, int RT, int PPW, int MAXC, bool REPLAY, bool ONE>
+int launch_gate_pp(const mcgmil::GateParams& gp, hipStream_t s) {
+    constexpr int BM = 16 * RT;
+    auto* k = &mcgmil::gate_pp_kernel<E, RT, PPW, MAXC, REPLAY, ONE>;
+    const long long tiles = (gp.total_samples + BM - 1) / BM;
+    if (tiles == 0) return MCGMIL_OK;
+    if (gp.uniform_rows <= 0)
+        if (int rc = launch_plan(gp, BM, s)) return rc;
+    const size_t lds = mcgmil::pp_lds_bytes<E, RT, MAXC>();
+    hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(mcgmil::kPPThreads), lds, s, gp);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_pp_kernel launch");
+}
+
+// Kernel choice for bf16 heads of up to 16 gate tile pairs (measured, config 3, MI355X):
+// separate heads (P = 16) run the one-workgroup-per-CU gate_pipe_kernel (914 vs 853 TFLOP/s),
+// shared heads (P = 8) the two-workgroups-per-CU gate_pp_kernel (820 vs 781).
+// MCGMIL_GATE=pipe / pp forces one of them (A/B timing).
+int gate_mode() {   // 0 auto, 1 pipe, 2 pp
+    static const int mode = [] {
+        const char* e = getenv("MCGMIL_GATE");
+        if (e && strcmp(e, "pipe") == 0) return 1;
+        if (e && strcmp(e, "pp") == 0) return 2;
+        return 0;
+    }();
+    return mode;
+}
+
+template <int RT, int PPW, int MAXC>
+int dispatch_gate_pp(const mcgmil::GateParams& gp, hipStream_t s) {
+    const bool replay = gp.keep_feat != nullptr;
+    const bool one = gp.G > 1 && gp.G == gp.C && (gp.D / 16) % PPW == 0;
+    if (replay) return one ? launch_gate_pp<__bf16, RT, PPW, MAXC, true, true>(gp, s)
+                           : launch_gate_pp<__bf16, RT, PPW, MAXC, true, false>(gp, s);
+    return one ? launch_gate_pp<__bf16, RT, PPW, MAXC, false, true>(gp, s)
+               : launch_gate_pp<__bf16, RT, PPW, MAXC, false, false>(gp, s);
+}
+
 template <typename E, int PPW, int MAXC>
 int dispatch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
     const bool replay = gp.keep_feat != nullptr;
@@ -182,6 +222,13 @@ int dispatch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
 template <typename E, int MAXC>
 int dispatch_gate_maxc(const mcgmil::GateParams& gp, int L, int dtype, hipStream_t s) {
     const bool pipe_ok = L % 64 == 0;          // the pipelined K loop is unrolled by two steps
+    if constexpr (sizeof(E) == 2) {
+        const int mode = gate_mode();
+        if (pipe_ok && mode != 1) {
+            if (gp.P <= 2 * mcgmil::kPPWaves) return dispatch_gate_pp<8, 2, MAXC>(gp, s);
+            if (mode == 2 && gp.P <= 4 * mcgmil::kPPWaves) return dispatch_gate_pp<4, 4, MAXC>(gp, s);
+        }
+    }
     if (pipe_ok && gp.P <= mcgmil::kGateWaves) return dispatch_gate_pipe<E, 1, MAXC>(gp, s);
     if (pipe_ok && gp.P <= 2 * mcgmil::kGateWaves) return dispatch_gate_pipe<E, 2, MAXC>(gp, s);
     // larger heads: whole masked tile in LDS, several passes of 16 pairs

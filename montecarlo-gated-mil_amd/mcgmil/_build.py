@@ -13,14 +13,21 @@ INCLUDE = os.path.join(os.path.dirname(ROOT), "include")
 LIB = os.path.join(PKG, "libmcgmil.so")
 SOURCES = ["mcgmil.hip", "mcgmil_image.hip"]
 DEPS = ["mcgmil.hip", "mcgmil_image.hip", "mcgmil_kernels.h", "mcgmil_device.h",
-        "mcgmil_error.h"]
+        "mcgmil_error.h", "mcgmil_gate_pp.h"]
 ARCH = os.environ.get("MCGMIL_OFFLOAD_ARCH", "gfx950")
+# No packed-fp32 VALU (v_pk_fma/mul/add_f32): with ROCm 7.2's compiler a packed write into the
+# source VGPR of a just-issued v_rcp_f32 / v_exp_f32 gets no wait states, and on gfx950 the
+# transcendental then sometimes reads the new value (nondeterministic low halves of the gate
+# epilogue, found by scripts/probe_determinism.py). Scalar fp32 VALU is hazard-checked.
+DEVICE_FLAGS = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 
 
 def _stale(out: str = LIB) -> bool:
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
+    if os.path.getmtime(os.path.abspath(__file__)) > t:      # build flags changed
+        return True
     deps = [os.path.join(CSRC, d) for d in DEPS] + \
         [os.path.join(INCLUDE, h) for h in ("mcgmil.h", "mcgmil_image.h")]
     return any(os.path.getmtime(d) > t for d in deps)
@@ -34,7 +41,7 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
     tmp = out + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall",
-           "-Werror", f"-I{INCLUDE}", "-o", tmp] + [f"-D{d}" for d in defines] + \
+           "-Werror", f"-I{INCLUDE}", "-o", tmp] + DEVICE_FLAGS + [f"-D{d}" for d in defines] + \
           [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd))

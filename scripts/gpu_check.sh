@@ -34,8 +34,12 @@ for s in $STEPS; do
         imgtests) run pytest_gpu_image 600 python -m pytest tests/test_gpu_image.py -m gpu -q -rf ;;
         imgprobe) run probe_image 300 python scripts/probe_image.py ;;
         e2etests) run pytest_gpu_pipeline 600 python -m pytest tests/test_gpu_pipeline.py -m gpu -q -rf ;;
+        resnet) run probe_resnet 600 python scripts/probe_resnet.py ;;
         cfg5) run bench_cfg5 900 python bench.py --workload cfg5 --steps 5 --warmup 2 ;;
         probe) run probe 300 python scripts/probe_gate.py ;;
+        determ) run determinism 300 python scripts/probe_determinism.py && \
+                run determinism_pipe 300 env MCGMIL_GATE=pipe python scripts/probe_determinism.py ;;
+        probepipe) run probe_pipe 300 env MCGMIL_GATE=pipe python scripts/probe_gate.py ;;
         stamps) run stamps 300 python scripts/probe_stamps.py ;;
         ab) run ab 300 env MCGMIL_PROBE_LIBS="$(ls -1 /tmp/mcgmil_var/*.so 2>/dev/null | paste -sd, -)" \
                 PROBE_ONLY=philox python scripts/probe_gate.py ;;
