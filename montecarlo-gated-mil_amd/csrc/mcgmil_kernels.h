@@ -162,11 +162,18 @@ __device__ __forceinline__ void fold_pairs(const GateParams& p, const f32x4 (&ac
         for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-                const float pr = gated_product_scaled(fmaf(acc[rt][2 * jp][v], av_s, bvv[v]),
-                                                      fmaf(acc[rt][2 * jp + 1][v], au_s, buv[v]));
+                const float ax = fmaf(acc[rt][2 * jp][v], av_s, bvv[v]);
+                const float by = fmaf(acc[rt][2 * jp + 1][v], au_s, buv[v]);
                 if constexpr (ONE_CLASS) {
-                    part[0][rt] = fmaf(pr, coef[0][v], part[0][rt]);
+                    // wa (1 - a) / ((1 + a)(1 + b)) as two FMAs around the reciprocal
+                    const float a = __builtin_amdgcn_exp2f(fminf(fmaxf(ax, -43.280851226668903f),
+                                                                 43.280851226668903f));
+                    const float b = __builtin_amdgcn_exp2f(by);
+                    const float ia = 1.0f + a;
+                    const float r = __builtin_amdgcn_rcpf(fmaf(ia, b, ia));
+                    part[0][rt] = fmaf(fmaf(-a, coef[0][v], coef[0][v]), r, part[0][rt]);
                 } else {
+                    const float pr = gated_product_scaled(ax, by);
 #pragma unroll
                     for (int c = 0; c < MAXC; ++c) part[c][rt] = fmaf(pr, coef[c][v], part[c][rt]);
                 }
