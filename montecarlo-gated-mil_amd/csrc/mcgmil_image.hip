@@ -29,6 +29,7 @@ using mcgmil::wave_max;
 constexpr int kThreads = 256;
 constexpr int kMaxStarts = 4096;     // tile start points per dimension
 constexpr int kMaxCover = 4096;      // instances covering one cell (LDS list)
+constexpr int kMaxSide = 65535;      // pixels per axis (grid_kernel's LDS byte map)
 constexpr uint32_t kShuffleTag = 0x5348464cu;   // "SHFL": Philox counter word of the shuffle
 
 // ---------------------------------------------------------------------------------------
@@ -94,6 +95,8 @@ int max_cover_1d(const std::vector<int32_t>& s, const std::vector<int32_t>& b, i
 int validate_geometry(const mcgmil_image_args* a, Geom* g, int* max_cover = nullptr) {
     if (!a) return fail(MCGMIL_E_INVALID, "args is NULL");
     if (a->height < 1 || a->width < 1) return fail(MCGMIL_E_INVALID, "image height/width must be >= 1");
+    if (a->height > kMaxSide || a->width > kMaxSide)
+        return fail(MCGMIL_E_UNSUPPORTED, "image sides above 65535 pixels are not built");
     if (a->patch_size < 1) return fail(MCGMIL_E_INVALID, "patch_size must be >= 1");
     if (a->patch_size > a->height || a->patch_size > a->width)
         return fail(MCGMIL_E_UNSUPPORTED, "patch_size larger than the image");
@@ -125,7 +128,7 @@ int validate_geometry(const mcgmil_image_args* a, Geom* g, int* max_cover = null
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct Layout {
-    size_t ys, xs, yb, xb, rowcell, colcell, counts, sorted, cellval, cellstat, total;
+    size_t ys, xs, yb, xb, rowcell, colcell, counts, sorted, rank, pos, above, cellval, cellstat, total;
 };
 
 Layout layout(const Geom& g, int T, int C) {
@@ -140,6 +143,9 @@ Layout layout(const Geom& g, int T, int C) {
     l.colcell = take(4 * (size_t)g.W);
     l.counts = take(4 * (size_t)g.tiles());
     l.sorted = take(4 * (size_t)g.tiles());
+    l.rank = take(4 * (size_t)g.tiles());
+    l.pos = take(4 * (size_t)g.tiles());
+    l.above = take(4);
     l.cellval = take(4 * (size_t)std::max(T, 0) * std::max(C, 0) * g.cells());
     l.cellstat = take(8 * (size_t)std::max(C, 0) * g.cells());
     l.total = o;
@@ -147,7 +153,7 @@ Layout layout(const Geom& g, int T, int C) {
 }
 
 struct Ws {
-    int32_t *ys, *xs, *yb, *xb, *rowcell, *colcell, *counts, *sorted;
+    int32_t *ys, *xs, *yb, *xb, *rowcell, *colcell, *counts, *sorted, *rank, *pos, *above;
     float *cellval, *cellstat;
 };
 
@@ -155,52 +161,68 @@ Ws carve(void* base, const Layout& l) {
     char* b = (char*)base;
     return Ws{(int32_t*)(b + l.ys), (int32_t*)(b + l.xs), (int32_t*)(b + l.yb), (int32_t*)(b + l.xb),
               (int32_t*)(b + l.rowcell), (int32_t*)(b + l.colcell), (int32_t*)(b + l.counts),
-              (int32_t*)(b + l.sorted), (float*)(b + l.cellval), (float*)(b + l.cellstat)};
+              (int32_t*)(b + l.sorted), (int32_t*)(b + l.rank), (int32_t*)(b + l.pos),
+              (int32_t*)(b + l.above), (float*)(b + l.cellval), (float*)(b + l.cellstat)};
 }
 
 // ---------------------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------------------
 
-// Grid setup. Blocks [0, by) map image rows to cells, blocks [by, by + bx) columns; each block
-// rebuilds its axis's starts and boundaries in LDS (a few hundred sequential steps) so no
-// block waits on another. Block 0 of each axis publishes the arrays; all blocks also zero the
-// tile counters.
-__global__ void __launch_bounds__(kThreads) grid_kernel(Geom g, int by, Ws w, int zero_counts) {
-    __shared__ int32_t s_starts[kMaxStarts];
-    __shared__ int32_t s_bounds[2 * kMaxStarts];
-    __shared__ int s_nb;
-    const bool rows = (int)blockIdx.x < by;
-    const int blk = rows ? blockIdx.x : blockIdx.x - by;
+// Grid setup, one 1024-thread block per axis (block 0: rows, block 1: columns). Every start
+// s_i and end s_i + ps is flagged in an LDS byte map over positions 0..size; a block-wide
+// prefix count over the map then yields the sorted, de-duplicated cell boundaries and the
+// cell index of every pixel (last boundary <= p) in one pass. The start points have a closed
+// form: s_i = i * stride for i < n - 1 and s_{n-1} = size - ps (image_patcher.py:16-28).
+constexpr int kGridThreads = 1024;
+
+__global__ void __launch_bounds__(kGridThreads) grid_kernel(Geom g, Ws w, int zero_counts) {
+    __shared__ uint8_t s_flag[kMaxSide + 1];
+    __shared__ int s_scan[kGridThreads / 64];
+    const bool rows = blockIdx.x == 0;
     const int size = rows ? g.H : g.W;
-    if (threadIdx.x == 0) {
-        const int n = start_points(size, g.ps, g.stride, s_starts);
-        s_nb = merge_bounds(s_starts, n, g.ps, s_bounds);
+    const int n = rows ? g.ny : g.nx;
+    int32_t* starts = rows ? w.ys : w.xs;
+    int32_t* bounds = rows ? w.yb : w.xb;
+    int32_t* cell = rows ? w.rowcell : w.colcell;
+    const int tid = threadIdx.x;
+    for (int q = tid; q <= size; q += kGridThreads) s_flag[q] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += kGridThreads) {
+        const int st = i < n - 1 ? i * g.stride : size - g.ps;
+        starts[i] = st;
+        s_flag[st] = 1;          // racing writes store the same value
+        s_flag[st + g.ps] = 1;
     }
     __syncthreads();
-    const int n = rows ? g.ny : g.nx;
-    const int nb = s_nb;
-    if (blk == 0) {
-        int32_t* starts = rows ? w.ys : w.xs;
-        int32_t* bounds = rows ? w.yb : w.xb;
-        for (int i = threadIdx.x; i < n; i += kThreads) starts[i] = s_starts[i];
-        for (int i = threadIdx.x; i < nb; i += kThreads) bounds[i] = s_bounds[i];
+    // chunk of positions per thread, its flag count, then a block-wide exclusive scan
+    const int chunk = (size + 1 + kGridThreads - 1) / kGridThreads;
+    const int q0 = tid * chunk, q1 = min(q0 + chunk, size + 1);
+    int cnt = 0;
+    for (int q = q0; q < q1; ++q) cnt += s_flag[q];
+    const int lane = tid & 63, wv = tid >> 6;
+    int incl = cnt;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
     }
-    const int p = blk * kThreads + threadIdx.x;
-    if (p < size) {   // cell = last boundary <= p (the final boundary == size is never <= p)
-        int lo = 0, hi = nb - 2;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_bounds[mid] <= p) lo = mid;
-            else hi = mid - 1;
-        }
-        (rows ? w.rowcell : w.colcell)[p] = lo;
+    if (lane == 63) s_scan[wv] = incl;
+    __syncthreads();
+    int base = 0;
+    for (int v = 0; v < wv; ++v) base += s_scan[v];
+    int running = base + incl - cnt;           // boundaries before this chunk
+    for (int q = q0; q < q1; ++q) {
+        if (s_flag[q]) bounds[running++] = q;
+        if (q < size) cell[q] = running - 1;
     }
-    if (zero_counts) {
+    if (zero_counts) {   // counters of the selection (cell_count, rank and order kernels)
         const long long nt = g.tiles();
-        for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < nt;
-             i += (long long)gridDim.x * kThreads)
+        for (long long i = (long long)blockIdx.x * kGridThreads + tid; i < nt; i += 2ll * kGridThreads) {
             w.counts[i] = 0;
+            w.rank[i] = 0;
+            w.pos[i] = 0;
+        }
+        if (blockIdx.x == 0 && tid == 0) *w.above = 0;
     }
 }
 
@@ -246,61 +268,82 @@ __device__ __forceinline__ float nonzero_percent(int count, float area) {
     return (float)count / area * 100.0f;   // == torch (mask.float().mean() * 100), fp32
 }
 
-// px, the kept count k and the stable rank order (px descending, tile index ascending):
-// tile i goes to position #{j : px_j > px_i or (px_j == px_i and j < i)} when that is < k.
-__global__ void __launch_bounds__(kThreads) select_kernel(Geom g, float thr, int cap, Ws w, float* px_out,
-                                                          int32_t* num_selected) {
+// Stable rank of every tile (px descending, tile index ascending), split over a 2-D grid:
+// block (bx, by) compares tiles bx*256.. against the j-chunk by*256.. and adds its partial
+// counts with integer atomics (order-independent). Blocks of column 0 also count the tiles
+// above the threshold, chunk by chunk.
+__global__ void __launch_bounds__(kThreads) rank_kernel(Geom g, float thr, Ws w) {
     __shared__ float s_px[kThreads];
+    __shared__ int s_above[kThreads / 64];
     const int nt = (int)g.tiles();
     const float area = (float)(g.ps * g.ps);   // numel of a tile
     const int i = blockIdx.x * kThreads + threadIdx.x;
-    const float pi = i < nt ? nonzero_percent(w.counts[i], area) : 0.f;
-    int rank = 0, above = 0;
-    for (int base = 0; base < nt; base += kThreads) {
-        __syncthreads();
-        const int j = base + threadIdx.x;
-        s_px[threadIdx.x] = j < nt ? nonzero_percent(w.counts[j], area) : -1.f;
-        __syncthreads();
-        const int m = min(kThreads, nt - base);
-        for (int jj = 0; jj < m; ++jj) {
-            const float pj = s_px[jj];
-            above += pj > thr;
-            rank += (pj > pi) || (pj == pi && base + jj < i);
-        }
+    const int base = blockIdx.y * kThreads;
+    const int j = base + threadIdx.x;
+    const float pj = j < nt ? nonzero_percent(w.counts[j], area) : -1.f;
+    s_px[threadIdx.x] = pj;
+    if (blockIdx.x == 0) {
+        const unsigned long long m = __ballot(j < nt && pj > thr);
+        if ((threadIdx.x & 63) == 0) s_above[threadIdx.x >> 6] = __popcll(m);
     }
-    const int k = min(above, cap);
-    if (i < nt) {
-        if (px_out) px_out[i] = pi;
-        if (rank < k) w.sorted[rank] = i;
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const int a = s_above[0] + s_above[1] + s_above[2] + s_above[3];
+        if (a) atomicAdd(w.above, a);
     }
+    if (i >= nt) return;
+    const float pi = nonzero_percent(w.counts[i], area);
+    const int m = min(kThreads, nt - base);
+    int rank = 0;
+    for (int jj = 0; jj < m; ++jj) {
+        const float q = s_px[jj];
+        rank += (q > pi) || (q == pi && base + jj < i);
+    }
+    if (rank) atomicAdd(w.rank + i, rank);
+}
+
+// px, k = min(#above, cap) and the rank-ordered tile list.
+__global__ void __launch_bounds__(kThreads) scatter_kernel(Geom g, int cap, Ws w, float* px_out,
+                                                           int32_t* num_selected) {
+    const int nt = (int)g.tiles();
+    const int i = blockIdx.x * kThreads + threadIdx.x;
+    const int k = min(*w.above, cap);
     if (i == 0) *num_selected = k;
+    if (i >= nt) return;
+    if (px_out) px_out[i] = nonzero_percent(w.counts[i], (float)(g.ps * g.ps));
+    const int r = w.rank[i];
+    if (r < k) w.sorted[r] = i;
 }
 
 // The bag order. shuffle: position of rank r = #{r' < k : key_r' < key_r or (== and r' < r)},
 // key_r = Philox4x32-10(counter {r, 0, 0, "SHFL"}, key = seed) word 0 -- a seeded permutation
-// standing in for sklearn.utils.shuffle (image_patcher.py:131).
-__global__ void __launch_bounds__(kThreads) order_kernel(Ws w, int shuffle, uint32_t k0, uint32_t k1,
-                                                         const int32_t* num_selected, int32_t* ids) {
+// standing in for sklearn.utils.shuffle (image_patcher.py:131). Same 2-D split as rank_kernel.
+__global__ void __launch_bounds__(kThreads) shuffle_rank_kernel(uint32_t k0, uint32_t k1,
+                                                                const int32_t* num_selected, Ws w) {
     __shared__ uint32_t s_key[kThreads];
     const int k = *num_selected;
+    const int base = blockIdx.y * kThreads;
+    if (base >= k) return;                       // uniform per block
+    const int j = base + threadIdx.x;
+    s_key[threadIdx.x] = philox4x32_10((uint32_t)j, 0u, 0u, kShuffleTag, k0, k1).x;
+    __syncthreads();
     const int r = blockIdx.x * kThreads + threadIdx.x;
-    if (!shuffle) {
-        if (r < k) ids[r] = w.sorted[r];
-        return;
-    }
+    if (r >= k) return;
     const uint32_t kr = philox4x32_10((uint32_t)r, 0u, 0u, kShuffleTag, k0, k1).x;
+    const int m = min(kThreads, k - base);
     int pos = 0;
-    for (int base = 0; base < k; base += kThreads) {
-        __syncthreads();
-        s_key[threadIdx.x] = philox4x32_10((uint32_t)(base + threadIdx.x), 0u, 0u, kShuffleTag, k0, k1).x;
-        __syncthreads();
-        const int m = min(kThreads, k - base);
-        for (int jj = 0; jj < m; ++jj) {
-            const uint32_t kj = s_key[jj];
-            pos += (kj < kr) || (kj == kr && base + jj < r);
-        }
+    for (int jj = 0; jj < m; ++jj) {
+        const uint32_t q = s_key[jj];
+        pos += (q < kr) || (q == kr && base + jj < r);
     }
-    if (r < k) ids[pos] = w.sorted[r];
+    if (pos) atomicAdd(w.pos + r, pos);
+}
+
+__global__ void __launch_bounds__(kThreads) order_kernel(Ws w, int shuffle, const int32_t* num_selected,
+                                                         int32_t* ids) {
+    const int k = *num_selected;
+    const int r = blockIdx.x * kThreads + threadIdx.x;
+    if (r < k) ids[shuffle ? w.pos[r] : r] = w.sorted[r];
 }
 
 template <typename Out> __device__ __forceinline__ Out to_out(float v);
@@ -317,14 +360,14 @@ struct Norm {
 // instances[n, ch, r, :] = image[ch, y + r, x : x + ps] for n < k (image_patcher.py:52, the
 // float copy new_img[i] = image[...] then new_img[sorted_idx]), optionally normalised per
 // channel as the dataset's T.Normalize does: (x - mean) / std in fp32 (utils.py:50-51).
-// One wave per row, VEC elements per lane (VEC = 4 when rows and tiles are 4-aligned).
+// 32 threads per tile row, VEC elements each (VEC = 8 when rows and tiles are 8-aligned), 8
+// rows per 256-thread block; rows of ps > 32*VEC loop.
 template <typename In, typename Out, int VEC>
 __global__ void __launch_bounds__(kThreads) gather_kernel(Geom g, int channels, const In* img,
                                                           long long ld_row, long long ld_ch, Ws w,
                                                           const int32_t* ids, const int32_t* num_selected,
                                                           Norm nm, Out* out) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const long long row = (long long)blockIdx.x * (kThreads / 64) + wave;   // over (n, ch, r)
+    const long long row = (long long)blockIdx.x * (kThreads / 32) + (threadIdx.x >> 5);   // (n, ch, r)
     const int ps = g.ps;
     const long long n = row / ((long long)channels * ps);
     if (n >= *num_selected) return;
@@ -335,7 +378,7 @@ __global__ void __launch_bounds__(kThreads) gather_kernel(Geom g, int channels, 
     const In* src = img + ch * ld_ch + (long long)(ty + r) * ld_row + tx;
     Out* dst = out + row * ps;
     const float m = nm.on ? nm.mean[ch] : 0.f, sd = nm.on ? nm.std[ch] : 1.f;
-    for (int x = lane * VEC; x < ps; x += 64 * VEC) {
+    for (int x = (threadIdx.x & 31) * VEC; x < ps; x += 32 * VEC) {
         const vec_t<In, VEC> v = *reinterpret_cast<const vec_t<In, VEC>*>(src + x);
         vec_t<Out, VEC> o;
 #pragma unroll
@@ -416,23 +459,34 @@ __global__ void __launch_bounds__(kThreads) normalize_kernel(Geom g, Ws w) {
 }
 
 // Mean and unbiased std over the T passes per (class, cell), accumulated in fp64
-// (infer.py:216-219; torch's CPU reductions accumulate float in double).
+// (infer.py:216-219). A block takes 64 (class, cell) items; its 4 waves split the passes and
+// combine their sums of v and v^2 in LDS (values lie in [0, 1]: no cancellation issue in fp64).
 __global__ void __launch_bounds__(kThreads) cell_stats_kernel(Geom g, int T, int C, Ws w) {
+    __shared__ double s_sum[kThreads / 64][64], s_sq[kThreads / 64][64];
     const long long cells = g.cells();
-    const long long i = (long long)blockIdx.x * kThreads + threadIdx.x;   // over (c, cell)
-    if (i >= C * cells) return;
-    const int c = (int)(i / cells);
-    const long long cell = i % cells;
-    double s = 0.0;
-    for (int t = 0; t < T; ++t) s += (double)w.cellval[((long long)t * C + c) * cells + cell];
-    const double mean = s / T;
-    double q = 0.0;
-    for (int t = 0; t < T; ++t) {
-        const double d = (double)w.cellval[((long long)t * C + c) * cells + cell] - mean;
-        q += d * d;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long long i = (long long)blockIdx.x * 64 + lane;    // over (c, cell)
+    double s = 0.0, q = 0.0;
+    if (i < C * cells) {
+        const int c = (int)(i / cells);
+        const long long cell = i % cells;
+        for (int t = wv; t < T; t += kThreads / 64) {
+            const double v = (double)w.cellval[((long long)t * C + c) * cells + cell];
+            s += v;
+            q += v * v;
+        }
     }
+    s_sum[wv][lane] = s;
+    s_sq[wv][lane] = q;
+    __syncthreads();
+    if (wv != 0 || i >= C * cells) return;
+    for (int k = 1; k < kThreads / 64; ++k) {
+        s += s_sum[k][lane];
+        q += s_sq[k][lane];
+    }
+    const double mean = s / T;
     w.cellstat[i] = (float)mean;
-    w.cellstat[C * cells + i] = T > 1 ? (float)sqrt(q / (T - 1)) : NAN;
+    w.cellstat[C * cells + i] = T > 1 ? (float)sqrt(fmax(q - s * mean, 0.0) / (T - 1)) : NAN;
 }
 
 // Expand per-cell planes to pixels: planes [0, P0) come from src0 into out0, planes [P0, P)
@@ -495,8 +549,7 @@ int check_launch(const char* what) {
 }
 
 int launch_grid(const Geom& g, const Ws& w, bool zero_counts, hipStream_t s) {
-    const int by = (g.H + kThreads - 1) / kThreads, bx = (g.W + kThreads - 1) / kThreads;
-    hipLaunchKernelGGL(grid_kernel, dim3(by + bx), dim3(kThreads), 0, s, g, by, w, zero_counts ? 1 : 0);
+    hipLaunchKernelGGL(grid_kernel, dim3(2), dim3(kGridThreads), 0, s, g, w, zero_counts ? 1 : 0);
     return check_launch("grid_kernel");
 }
 
@@ -518,7 +571,7 @@ int launch_count(const Geom& g, const mcgmil_image_args* a, const Ws& w, hipStre
 template <typename In, typename Out>
 int launch_gather(const Geom& g, const mcgmil_image_args* a, const Ws& w, hipStream_t s) {
     const long long rows = (long long)a->instance_capacity * a->channels * g.ps;
-    const long long blocks = (rows + kThreads / 64 - 1) / (kThreads / 64);
+    const long long blocks = (rows + kThreads / 32 - 1) / (kThreads / 32);
     if (blocks == 0) return MCGMIL_OK;
     Norm nm;
     nm.on = a->normalize ? 1 : 0;
@@ -526,13 +579,13 @@ int launch_gather(const Geom& g, const mcgmil_image_args* a, const Ws& w, hipStr
         nm.mean[c] = a->norm_mean[c];
         nm.std[c] = a->norm_std[c];
     }
-    // 4-wide when every tile row starts 4-aligned: base, strides, tile starts and ps
-    const bool vec4 = ((uintptr_t)a->image % (4 * sizeof(In))) == 0 && a->ld_row % 4 == 0 &&
-                      (a->channels == 1 || a->ld_channel % 4 == 0) && g.ps % 4 == 0 && g.stride % 4 == 0 &&
-                      (g.W - g.ps) % 4 == 0 && ((uintptr_t)a->instances % 16) == 0;
+    // 8-wide when every tile row starts 8-aligned: base, strides, tile starts and ps
+    const bool vec8 = ((uintptr_t)a->image % (8 * sizeof(In))) == 0 && a->ld_row % 8 == 0 &&
+                      (a->channels == 1 || a->ld_channel % 8 == 0) && g.ps % 8 == 0 && g.stride % 8 == 0 &&
+                      (g.W - g.ps) % 8 == 0 && ((uintptr_t)a->instances % (8 * sizeof(Out))) == 0;
     const dim3 grid((unsigned)blocks), block(kThreads);
-    if (vec4)
-        hipLaunchKernelGGL((gather_kernel<In, Out, 4>), grid, block, 0, s, g, a->channels, (const In*)a->image,
+    if (vec8)
+        hipLaunchKernelGGL((gather_kernel<In, Out, 8>), grid, block, 0, s, g, a->channels, (const In*)a->image,
                            (long long)a->ld_row, (long long)a->ld_channel, w, a->tile_ids, a->num_selected, nm,
                            (Out*)a->instances);
     else
@@ -599,7 +652,8 @@ int mcgmil_image_to_bag(const mcgmil_image_args* a, void* stream) {
     if (a->ld_row < a->width || (a->channels > 1 && a->ld_channel < (int64_t)a->height * a->ld_row))
         return fail(MCGMIL_E_INVALID, "image strides too small");
     const long long nt = g.tiles();
-    if (nt > 0x7fffffffll) return fail(MCGMIL_E_UNSUPPORTED, "too many tiles");
+    // the O(n^2) ranking runs as a (n/256)^2 grid: cap n at 2^20 tiles (a 16k x 16k image at ps 16)
+    if (nt > (1ll << 20)) return fail(MCGMIL_E_UNSUPPORTED, "more than 2^20 tiles");
     const int cap = a->bag_size > 0 ? a->bag_size : 0x7fffffff;
     if (a->instances) {
         if (a->normalize && a->channels > 4) return fail(MCGMIL_E_UNSUPPORTED, "normalize supports c <= 4");
@@ -622,10 +676,17 @@ int mcgmil_image_to_bag(const mcgmil_image_args* a, void* stream) {
     if (rc) return rc;
     const float thr = (float)(a->empty_thresh * 100.0);   // torch: fp32 tensor > python float
     const unsigned tb = (unsigned)((nt + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL(select_kernel, dim3(tb), dim3(kThreads), 0, s, g, thr, cap, w, a->px, a->num_selected);
-    if ((rc = check_launch("select_kernel"))) return rc;
-    hipLaunchKernelGGL(order_kernel, dim3(tb), dim3(kThreads), 0, s, w, a->shuffle ? 1 : 0,
-                       (uint32_t)a->shuffle_seed, (uint32_t)(a->shuffle_seed >> 32), a->num_selected, a->tile_ids);
+    hipLaunchKernelGGL(rank_kernel, dim3(tb, tb), dim3(kThreads), 0, s, g, thr, w);
+    if ((rc = check_launch("rank_kernel"))) return rc;
+    hipLaunchKernelGGL(scatter_kernel, dim3(tb), dim3(kThreads), 0, s, g, cap, w, a->px, a->num_selected);
+    if ((rc = check_launch("scatter_kernel"))) return rc;
+    if (a->shuffle) {
+        hipLaunchKernelGGL(shuffle_rank_kernel, dim3(tb, tb), dim3(kThreads), 0, s, (uint32_t)a->shuffle_seed,
+                           (uint32_t)(a->shuffle_seed >> 32), a->num_selected, w);
+        if ((rc = check_launch("shuffle_rank_kernel"))) return rc;
+    }
+    hipLaunchKernelGGL(order_kernel, dim3(tb), dim3(kThreads), 0, s, w, a->shuffle ? 1 : 0, a->num_selected,
+                       a->tile_ids);
     if ((rc = check_launch("order_kernel"))) return rc;
     if (!a->instances) return MCGMIL_OK;
     switch (it) {
@@ -661,7 +722,7 @@ int mcgmil_attention_maps(const mcgmil_image_args* a, void* stream) {
     if ((rc = check_launch("normalize_kernel"))) return rc;
     const bool stats = a->map_mean || a->map_std;
     if (stats) {
-        const unsigned sb = (unsigned)((a->C * g.cells() + kThreads - 1) / kThreads);
+        const unsigned sb = (unsigned)((a->C * g.cells() + 63) / 64);
         hipLaunchKernelGGL(cell_stats_kernel, dim3(sb), dim3(kThreads), 0, s, g, a->T, a->C, w);
         if ((rc = check_launch("cell_stats_kernel"))) return rc;
     }

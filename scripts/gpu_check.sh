@@ -46,14 +46,28 @@ for s in $STEPS; do
         prof)
             rm -rf "$OUT/prof_$TAG"
             run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run \
-                --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
+                --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline
             find "$OUT/prof_$TAG" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_$TAG.csv" \;
+            ;;
+        pmcsq)
+            rm -rf "$OUT/pmc_${TAG}_sq"
+            run pmc_sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+                SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES --kernel-trace \
+                -d "$OUT/pmc_${TAG}_sq" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
+            f=$(find "$OUT/pmc_${TAG}_sq" -name "*counter_collection.csv" | head -1)
+            python3 scripts/pmc_summary.py "$f" > "$OUT/pmc_sq_summary_$TAG.json"
+            ;;
+        profcfg5)
+            rm -rf "$OUT/prof_cfg5_$TAG"
+            run rocprof_cfg5 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg5_$TAG" -o run \
+                --output-format csv -- python3 bench.py --workload cfg5 --steps 5 --warmup 2 --no-cpu-baseline
+            find "$OUT/prof_cfg5_$TAG" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_cfg5_$TAG.csv" \;
             ;;
         pmc)
             for ctr in FETCH_SIZE WRITE_SIZE; do
                 rm -rf "$OUT/pmc_${TAG}_$ctr"
                 run pmc_$ctr 600 rocprofv3 --pmc $ctr --kernel-trace -d "$OUT/pmc_${TAG}_$ctr" -o run \
-                    --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline
+                    --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
                 find "$OUT/pmc_${TAG}_$ctr" -name "*counter_collection.csv" -exec cp {} "$OUT/pmc_${TAG}_$ctr.csv" \;
             done
             ;;

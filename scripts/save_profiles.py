@@ -22,7 +22,12 @@ def main(tag):
     ks = os.path.join(OUT, f"kernel_stats_{tag}.csv")
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(dst, "kernel_stats.csv"))
-    for name in ("bench.log", "rocprof.log", "probe.log", "stamps.log", "ab.log"):
+    for src, name in ((f"kernel_stats_cfg5_{tag}.csv", "kernel_stats_cfg5.csv"),
+                      (f"pmc_sq_summary_{tag}.json", "pmc_sq_summary.json")):
+        if os.path.exists(os.path.join(OUT, src)):
+            shutil.copy(os.path.join(OUT, src), os.path.join(dst, name))
+    for name in ("bench.log", "rocprof.log", "probe.log", "stamps.log", "ab.log", "bench_cfg5.log",
+                 "probe_image.log", "pytest_gpu.log", "smoke.log", "determinism.log"):
         p = os.path.join(OUT, name)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, name))

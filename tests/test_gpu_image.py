@@ -122,6 +122,26 @@ def test_fused_normalize(cuda, seed, out):
     assert torch.equal(inst.cpu(), want)
 
 
+@pytest.mark.parametrize("src_dtype,out", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                           (torch.uint8, torch.bfloat16), (torch.bfloat16, torch.float32)])
+def test_gather_wide_path(cuda, src_dtype, out):
+    """8-aligned geometry (W - ps and the stride multiples of 8): the 8-wide gather path."""
+    from mcgmil.patcher import ImagePatcher
+    h, w = 600, 456
+    img = synthetic_image(21, h, w, 3)
+    src = torch.from_numpy(img) if src_dtype != torch.uint8 else torch.from_numpy((img * 200).astype(np.uint8))
+    src = src.to(src_dtype)
+    ref = src.float()
+    p = ImagePatcher(patch_size=64, overlap=0.5, empty_thresh=0.3)
+    tiles = p.get_tiles(h, w)
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    inst, idx, _ = p.convert_img_to_bag(src.to(cuda), shuffle=False, out_dtype=out, normalize=(mean, std))
+    m = torch.tensor(mean)[:, None, None]
+    sd = torch.tensor(std)[:, None, None]
+    want = torch.stack([x.sub(m).div(sd) for x in P.crops(ref, tiles, idx)]).to(out)
+    assert len(idx) > 10 and torch.equal(inst.cpu(), want)
+
+
 def test_empty_and_capped_bags(cuda):
     from mcgmil.patcher import ImagePatcher
     p = ImagePatcher(patch_size=32, overlap=0.5, bag_size=-1, empty_thresh=0.5)
@@ -210,6 +230,7 @@ def test_config5_scale(cuda):
     px = P.nonzero_percent(img, tiles)
     assert torch.equal(p.last_px.cpu(), px)
     assert sorted(idx.tolist()) == sorted(P.select(px, 0.5, -1).tolist())
+    assert torch.equal(inst[:24].cpu(), P.crops(img, tiles, idx[:24]))       # 8-wide gather
     k = len(idx)
     assert k > 100
     T, C = 100, 2
