@@ -188,7 +188,11 @@ __global__ __launch_bounds__(kPPThreads, 2) void gate_pp_kernel(const GateParams
     __syncthreads();
     MCGMIL_STAMP(p, 2);
 
-    for (int s = 0; s < KS; s += 2) {   // KS is even (host guarantees L % 64 == 0)
+    // KS is even and >= 2 (host guarantees L % 64 == 0); the first two steps are peeled so their
+    // MFMAs take the zero accumulators as an inline constant (no copies into the loop).
+    kstep(0, Xs, Xs + SLOT, wA, wB, zA, zB, hB, hA);
+    kstep(1, Xs + SLOT, Xs, wB, wA, zB, zA, hA, hB);
+    for (int s = 2; s < KS; s += 2) {
         kstep(s, Xs, Xs + SLOT, wA, wB, zA, zB, hB, hA);
         kstep(s + 1, Xs + SLOT, Xs, wB, wA, zB, zA, hA, hB);
     }

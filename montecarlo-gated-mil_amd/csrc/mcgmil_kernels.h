@@ -488,7 +488,12 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     __syncthreads();
     MCGMIL_STAMP(p, 2);
 
-    for (int s = 0; s < KS; s += 2) {     // KS is even (host guarantees L % 64 == 0)
+    // KS is even and >= 2 (host guarantees L % 64 == 0). The first two steps are peeled: their
+    // MFMAs take the zero accumulators as an inline-constant C operand, so no register copies of
+    // the 132 zeroed accumulators are made on the way into the loop.
+    kstep(0, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA);
+    kstep(1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB);
+    for (int s = 2; s < KS; s += 2) {
         kstep(s, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA);
         kstep(s + 1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB);
     }
