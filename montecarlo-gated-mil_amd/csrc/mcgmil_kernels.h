@@ -77,13 +77,24 @@ __device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0
     if (tid >= BM) return;
     const long long R = R0 + tid;
     int hrow = -1, t = 0, n = 0, bag = 0, Nb = 0;
+    // 32-bit unsigned division when the launch's sample rows fit (wave-uniform branch); the
+    // 64-bit one is a ~50-instruction software routine
+    const bool narrow = p.total_samples <= 0xFFFFFFFFll;
     if (R < p.total_samples && p.uniform_rows > 0) {
         const long long per_bag = (long long)p.T * p.uniform_rows;
-        bag = (int)(R / per_bag);
         Nb = p.uniform_rows;
-        const long long local = R - (long long)bag * per_bag;
-        t = (int)(local / Nb);
-        n = (int)(local - (long long)t * Nb);
+        if (narrow) {
+            const uint32_t r = (uint32_t)R, pb = (uint32_t)per_bag;
+            bag = (int)(r / pb);
+            const uint32_t local = r - (uint32_t)bag * pb;
+            t = (int)(local / (uint32_t)Nb);
+            n = (int)(local - (uint32_t)t * (uint32_t)Nb);
+        } else {
+            bag = (int)(R / per_bag);
+            const long long local = R - (long long)bag * per_bag;
+            t = (int)(local / Nb);
+            n = (int)(local - (long long)t * Nb);
+        }
         hrow = bag * Nb + n;
     } else if (R < p.total_samples) {
         if (p.tile_bag) {
@@ -95,8 +106,13 @@ __device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0
         const int ob = p.bag_off[bag];
         Nb = p.bag_off[bag + 1] - ob;
         const long long local = R - (long long)p.T * ob;
-        t = (int)(local / Nb);
-        n = (int)(local - (long long)t * Nb);
+        if (narrow) {
+            t = (int)((uint32_t)local / (uint32_t)Nb);
+            n = (int)((uint32_t)local - (uint32_t)t * (uint32_t)Nb);
+        } else {
+            t = (int)(local / Nb);
+            n = (int)(local - (long long)t * Nb);
+        }
         hrow = ob + n;
     }
     int* ri = rinfo + kRowInfo * tid;
@@ -332,6 +348,7 @@ constexpr int VPM = MCGMIL_VPM;   // VALU instructions scheduled after each MFMA
 #ifndef MCGMIL_SCHED
 #define MCGMIL_SCHED 0
 #endif
+constexpr int HD = 2;               // H prefetch distance of the pipelined kernel, in K steps
 
 template <typename E, int MAXC>
 __host__ __device__ constexpr size_t pipe_lds_bytes() {
@@ -415,19 +432,16 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     f32x4 zacc = {0.f, 0.f, 0.f, 0.f};
 
     // One K step: MFMAs on step s from slot `cur` with weights (w, z); meanwhile prefetch the
-    // weights of step s+1 into (wn, zn) and the H chunk of step s+2 into hn, and stage step
+    // weights of step s+1 into (wn, zn) and the H chunk of step s+HD into hn, and stage step
     // s+1 (from h, loaded one step earlier) into slot `nxt`. Loop-carried values alternate
     // between two NAMED register sets (the loop is unrolled by two), so no register copy
     // forces an early wait on the prefetches.
+    // (The compiler issues the prefetches late in the step, next to the barrier. Forcing them
+    // to the top of the step or after the first 2-12 MFMAs measured 2-4% slower.)
     auto kstep = [&](int s, const E* cur, E* nxt, const Frag<E> (&w)[NJ], const Frag<E>& z,
                      Frag<E> (&wn)[NJ], Frag<E>& zn, const Raw<E>& h, Raw<E>& hn) {
         const int s1 = s + 1 < KS ? s + 1 : KS - 1;          // clamped: no branch in the body
-        const int s2 = s + 2 < KS ? s + 2 : KS - 1;
-#if MCGMIL_DIAG & 1   // ablation (timing only, wrong results): no H prefetch
-        hn = h;
-#else
-        hn = load_raw(hsrc + (size_t)s2 * 32);
-#endif
+        const int sh = s + HD < KS ? s + HD : KS - 1;
 #if MCGMIL_DIAG & 2   // ablation: no weight prefetch
 #pragma unroll
         for (int j = 0; j < NJ; ++j) wn[j] = w[j];
@@ -436,6 +450,11 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
 #pragma unroll
         for (int j = 0; j < NJ; ++j) wn[j] = wfrag(wsoff[j] + (uint32_t)s1 * kStepBytes);
         zn = wfrag(zsoff + (uint32_t)s1 * kStepBytes);
+#endif
+#if MCGMIL_DIAG & 1   // ablation (timing only, wrong results): no H prefetch
+        hn = h;
+#else
+        hn = load_raw(hsrc + (size_t)sh * 32);
 #endif
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
@@ -476,15 +495,15 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
         __syncthreads();
     };
 
-    // prologue: stage step 0, load H of step 1 and the weights of step 0
+    // prologue: stage step 0, load the weights of step 0 and H of step 1
     Frag<E> wA[NJ], wB[NJ], zA, zB;
     Raw<E> hA, hB;
     hA = load_raw(hsrc);
-    stage(0, hA, Xs);
-    hB = load_raw(hsrc + 32);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) wA[j] = wfrag(wsoff[j]);
     zA = wfrag(zsoff);
+    hB = load_raw(hsrc + 32);
+    stage(0, hA, Xs);
     __syncthreads();
     MCGMIL_STAMP(p, 2);
 

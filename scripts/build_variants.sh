@@ -1,15 +1,24 @@
 #!/bin/bash
-# Build A/B variants of libmcgmil.so into /tmp/mcgmil_var/ (one per -D set), in parallel.
+# Build A/B variants of libmcgmil.so (one per -D set), in parallel, into $VAR_OUT (default
+# build/var/, git-ignored but shipped to the GPU box with the snapshot).
 # Usage: bash scripts/build_variants.sh "NAME:-DX=1 -DY=2" "NAME2:..." ...
+#   A NAME of the form "name@REV" builds the sources of git revision REV instead of the tree.
 set -e
-mkdir -p /tmp/mcgmil_var
-rm -f /tmp/mcgmil_var/*.so
+OUT=${VAR_OUT:-build/var}
+mkdir -p "$OUT"
+rm -f "$OUT"/*.so
 for spec in "$@"; do
     name=${spec%%:*}; defs=${spec#*:}
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -Iinclude \
+    src=montecarlo-gated-mil_amd/csrc; inc=include
+    if [[ $name == *@* ]]; then
+        rev=${name#*@}; name=${name%@*}
+        tmp=$(mktemp -d)
+        git archive "$rev" montecarlo-gated-mil_amd/csrc include | tar -x -C "$tmp"
+        src=$tmp/montecarlo-gated-mil_amd/csrc; inc=$tmp/include
+    fi
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -I"$inc" \
         -Xclang -target-feature -Xclang -packed-fp32-ops $defs \
-        -o /tmp/mcgmil_var/$name.so montecarlo-gated-mil_amd/csrc/mcgmil.hip \
-        montecarlo-gated-mil_amd/csrc/mcgmil_image.hip &
+        -o "$OUT/$name.so" "$src/mcgmil.hip" "$src/mcgmil_image.hip" 2>&1 | grep -v packed-fp32-ops || true &
 done
 wait
-ls /tmp/mcgmil_var
+ls "$OUT"
