@@ -98,7 +98,7 @@ __device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0
         hrow = bag * Nb + n;
     } else if (R < p.total_samples) {
         if (p.tile_bag) {
-            bag = p.tile_bag[blockIdx.x];
+            bag = p.tile_bag[R0 / BM];
             while ((long long)p.T * p.bag_off[bag + 1] <= R) ++bag;
         } else {
             bag = find_bag(p.bag_off, p.B, p.T, R);
