@@ -7,6 +7,8 @@ HIP kernels behind the C ABI in include/mcgmil.h (libmcgmil.so, loaded with ctyp
   model.MultiHeadGatedAttentionMIL   the reference nn.Module API (ctor, state_dict, forward,
                                      mc_inference, mc_inference_serial) + mc_inference_features
   ops.mcdo_forward                   batched varlen entry (many bags x T samples, one launch)
+  library                            torch.ops.mcgmil.mcdo_forward(_stats): the same entry as
+                                     torch.library custom ops (fake kernels for graph capture)
   infer.mc_predict_bags              caller-side uncertainty summary (reference infer.py)
   shard                              bag sharding + prediction gather across GPUs
   resnet                             in-repo ResNet backbone (torchvision is not available)

@@ -169,6 +169,29 @@ def test_varlen_batch_matches_per_bag_oracle(cuda):
         assert nrel(Am[b].numpy().reshape(C, n), Ar[:, 0].mean(0).numpy()) <= 1e-5
 
 
+def test_torch_library_op_matches_ops(cuda):
+    """torch.ops.mcgmil.mcdo_forward(_stats) (SURVEY §8(b) custom-op registration) runs the same
+    kernels as ops.mcdo_forward: bitwise equal outputs, incl. a seed above 2^63."""
+    from mcgmil import library, ops  # noqa: F401  (registers torch.ops.mcgmil.*)
+    sizes = [64, 37, 300]
+    T, C, L, D = 4, 2, 512, 128
+    sd = synthetic.head_state_dict(5, L=L, D=D, C=C, shared=False)
+    head = head_on(synthetic.head_arrays(sd, C, False), cuda)
+    H = torch.from_numpy(np.concatenate([synthetic.bag_features(7 + b, n, L)
+                                         for b, n in enumerate(sizes)])).to(cuda).bfloat16()
+    offs = ops.bag_offsets_tensor(sizes, cuda)
+    seed = (1 << 63) + 12345
+    ref = ops.mcdo_forward(H, offs, head, T, p_feat=0.1, p_att=0.1, seed=seed, bag_id_base=3,
+                           return_stats=True)
+    signed = seed - (1 << 64)
+    Y, A = torch.ops.mcgmil.mcdo_forward(H, offs, *head, T, 0.1, 0.1, signed, 3, 0)
+    assert torch.equal(Y, ref["Y"]) and torch.equal(A, ref["A"])
+    Y2, Am, Av, Pm = torch.ops.mcgmil.mcdo_forward_stats(H, offs, *head, T, 0.1, 0.1, signed, 3, 0)
+    assert torch.equal(Y2, ref["Y"]) and torch.equal(Am, ref["A_mean"])
+    assert torch.equal(Av.isnan(), ref["A_var"].isnan())
+    assert torch.equal(Av.nan_to_num(), ref["A_var"].nan_to_num()) and torch.equal(Pm, ref["P_mean"])
+
+
 def test_shard_with_bag_ids_is_bitwise_rank_independent(cuda):
     """A subset of the batch run with its global bag ids reproduces the full batch bit for bit
     (what makes 1/2/4/8-GPU sharding results identical)."""

@@ -72,3 +72,32 @@ def test_bag_offsets_validation():
     assert ops.bag_offsets_tensor([3, 0, 5], "cpu").tolist() == [0, 3, 3, 8]
     with pytest.raises(ValueError):
         ops.bag_offsets_tensor([0, 5, 3], "cpu", are_sizes=False)
+
+
+def test_torch_library_ops_registered_with_fake_shapes():
+    """The custom ops are registered; their fake kernels give the output shapes
+    without touching a device, so graph captures can trace through them."""
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from mcgmil import library  # noqa: F401
+    assert hasattr(torch.ops.mcgmil, "mcdo_forward") and hasattr(torch.ops.mcgmil, "mcdo_forward_stats")
+    R, L, D, C, G, T, B = 300, 512, 128, 2, 2, 7, 3
+    with FakeTensorMode():
+        H = torch.empty(R, L, dtype=torch.bfloat16)
+        offs = torch.empty(B + 1, dtype=torch.int32)
+        head = (torch.empty(G, D, L), torch.empty(G, D), torch.empty(G, D, L), torch.empty(G, D),
+                torch.empty(C, D), torch.empty(C), torch.empty(C, L))
+        Y, A = torch.ops.mcgmil.mcdo_forward(H, offs, *head, T, 0.1, 0.1, 5, 0, 0)
+        Y2, Am, Av, Pm = torch.ops.mcgmil.mcdo_forward_stats(H, offs, *head, T, 0.1, 0.1, 5, 0, 0)
+    assert tuple(Y.shape) == (B, T, C) and tuple(A.shape) == (T * C * R,) and A.dtype == torch.float32
+    assert tuple(Y2.shape) == (B, T, C) and tuple(Am.shape) == tuple(Av.shape) == (C * R,)
+    assert tuple(Pm.shape) == (B, C)
+
+
+def test_torch_library_op_has_no_cpu_path():
+    from mcgmil import library  # noqa: F401
+    R, L, D, C = 8, 64, 16, 2
+    head = (torch.zeros(C, D, L), torch.zeros(C, D), torch.zeros(C, D, L), torch.zeros(C, D),
+            torch.zeros(C, D), torch.zeros(C), torch.zeros(C, L))
+    with pytest.raises(ValueError, match="CUDA"):
+        torch.ops.mcgmil.mcdo_forward(torch.zeros(R, L), torch.tensor([0, R], dtype=torch.int32),
+                                      *head, 2, 0.1, 0.1, 1, 0, 0)
