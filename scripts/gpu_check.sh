@@ -36,6 +36,9 @@ for s in $STEPS; do
         e2etests) run pytest_gpu_pipeline 600 python -m pytest tests/test_gpu_pipeline.py -m gpu -q -rf ;;
         resnet) run probe_resnet 600 python scripts/probe_resnet.py ;;
         cfg5) run bench_cfg5 900 python bench.py --workload cfg5 --steps 5 --warmup 2 ;;
+        cfg4) run bench_cfg4 600 python bench.py --workload cfg4 ;;
+        dist1) run bench_dist1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+                --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 5 --warmup 2 ;;
         probe) run probe 300 python scripts/probe_gate.py ;;
         determ) run determinism 300 python scripts/probe_determinism.py && \
                 run determinism_pipe 300 env MCGMIL_GATE=pipe python scripts/probe_determinism.py ;;
@@ -46,7 +49,7 @@ for s in $STEPS; do
         prof)
             rm -rf "$OUT/prof_$TAG"
             run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run \
-                --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline
+                --output-format csv -- python3 bench.py
             find "$OUT/prof_$TAG" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_$TAG.csv" \;
             ;;
         pmcsq)

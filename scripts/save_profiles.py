@@ -27,6 +27,7 @@ def main(tag):
         if os.path.exists(os.path.join(OUT, src)):
             shutil.copy(os.path.join(OUT, src), os.path.join(dst, name))
     for name in ("bench.log", "rocprof.log", "probe.log", "stamps.log", "ab.log", "bench_cfg5.log",
+                 "bench_cfg4.log", "bench_dist1.log", "rocprof_cfg5.log",
                  "probe_image.log", "pytest_gpu.log", "smoke.log", "determinism.log"):
         p = os.path.join(OUT, name)
         if os.path.exists(p):
