@@ -1,0 +1,75 @@
+/* mcgmil_features.h -- C ABI of the feature extractor's normalisation layers (SURVEY.md §8(f)
+ * row 1: the ResNet backbone that feeds the MCDO kernel, with BatchNorm on the bag's own batch
+ * statistics). libmcgmil.so exports these next to include/mcgmil.h.
+ *
+ * Reference interface replaced:
+ *   mcgmil_batchnorm_act   torch.nn.BatchNorm2d.forward of the backbone's BN layers
+ *                          (torchvision BasicBlock/Bottleneck as built at model.py:166-177),
+ *                          with the ReLU / residual add / stem max-pool that follows them, after
+ *                          deactivate_batchnorm (infer.py:105-109: track_running_stats=False,
+ *                          running stats None -> every forward normalises with the statistics
+ *                          of the bag itself)
+ *
+ * Layout: activations are channels-last (NHWC), i.e. a row-major [rows = N*H*W, C] matrix;
+ * C a multiple of 8, rows >= 1, x / residual / y 16-byte aligned.
+ *
+ * Semantics (torch.nn.functional.batch_norm + relu):
+ *   batch statistics (mean == var == NULL): mean_c = (1/rows) sum x[:, c],
+ *     var_c = (1/rows) sum (x[:, c] - mean_c)^2 (biased, as torch normalises in training mode),
+ *     accumulated in fp32 per workgroup around a per-channel shift (x[0, c]) and combined in fp64;
+ *   running statistics (both given): mean_c, var_c as passed;
+ *   y = x * a_c + b_c [+ residual] [then max(., 0)], with a_c = gamma_c / sqrt(var_c + eps) and
+ *     b_c = beta_c - mean_c * a_c in fp32 (gamma = 1, beta = 0 when NULL); one rounding to the
+ *     output dtype. torch rounds the BN output before the residual add; the fused form rounds
+ *     once (<= 1 bf16 ulp apart).
+ *   pooling (the torchvision stem, maxpool(relu(bn1(conv1(x))))): y[n, oh, ow, c] = max over the
+ *     window of the activated values, computed from x without materialising them (rounding is
+ *     monotonic, so this equals pooling the rounded activations); no residual with pooling.
+ * y may alias x (in place) without pooling. Stream-ordered, no allocation, no host
+ * synchronisation; errors are MCGMIL_E_* codes with mcgmil_last_error().
+ */
+#ifndef MCGMIL_FEATURES_H_
+#define MCGMIL_FEATURES_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mcgmil.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mcgmil_bn_args {
+    int64_t rows;               /* N * H * W */
+    int32_t channels;           /* C, multiple of 8, <= 4096 */
+    int32_t dtype;              /* MCGMIL_BF16 or MCGMIL_F32 (x, residual and y) */
+    const void* x;              /* [rows, C] */
+    const void* residual;       /* [rows, C] added before the activation, or NULL */
+    void* y;                    /* [rows, C], may alias x */
+    const float* gamma;         /* [C] BN weight or NULL (1) */
+    const float* beta;          /* [C] BN bias or NULL (0) */
+    const float* running_mean;  /* [C]: running-statistics mode when both are given */
+    const float* running_var;   /* [C] */
+    double eps;                 /* BN eps (torch default 1e-5) */
+    int32_t relu;               /* 1: max(., 0) after the (residual) add */
+    int32_t batch, height, width;   /* N, H, W with rows == N * H * W (needed with pooling) */
+    int32_t pool_kernel;        /* 0: none; k > 0: max-pool k x k after the activation */
+    int32_t pool_stride, pool_pad;  /* torch MaxPool2d(k, stride, pad): -inf padding, floor mode;
+                                       y is then [N * Ho * Wo, C], Ho = (H + 2 pad - k) / stride + 1 */
+    int32_t reserved;
+    float* batch_mean;          /* optional out [C]: the mean used */
+    float* batch_invstd;        /* optional out [C]: 1 / sqrt(var + eps) */
+    void* workspace;            /* >= mcgmil_bn_workspace_size() bytes, 256-byte aligned */
+    size_t workspace_bytes;
+} mcgmil_bn_args;
+
+size_t mcgmil_bn_args_size(void);   /* sizeof(mcgmil_bn_args), for binding checks */
+int mcgmil_bn_workspace_size(const mcgmil_bn_args* a, size_t* bytes);
+int mcgmil_batchnorm_act(const mcgmil_bn_args* a, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MCGMIL_FEATURES_H_ */

@@ -1,0 +1,385 @@
+// Feature-extractor normalisation (include/mcgmil_features.h): BatchNorm2d on the bag's own
+// batch statistics (reference infer.py:105-109 deactivate_batchnorm; the backbone of
+// model.py:166-177) fused with the ReLU / residual add that follows it in the ResNet blocks.
+//
+// Channels-last activations are a [rows, C] matrix. Three launches per layer:
+//   bn_partial_kernel   per-workgroup fp32 sums of (x - shift_c) and its square, shift_c = x[0, c]
+//                       (keeps E[x^2] - E[x]^2 well conditioned), 16-byte loads, LDS reduction
+//   bn_finalize_kernel  fp64 combination of the partials in a fixed order (deterministic), then
+//                       a_c = gamma_c / sqrt(var_c + eps), b_c = beta_c - mean_c * a_c
+//   bn_apply_kernel     y = x * a_c + b_c (+ residual) (relu), 16-byte loads and stores
+// HBM-bound elementwise/reduction work: two reads of x, one write of y (+ the residual read).
+// Replaces MIOpen's training-mode BN (mean/variance + normalise) and the separate add / clamp
+// kernels PyTorch runs for the same layers.
+#include <math.h>
+
+#include <numeric>
+#include <string>
+
+#include "../../include/mcgmil_features.h"
+#include "mcgmil_device.h"
+#include "mcgmil_error.h"
+
+namespace {
+
+using mcgmil_detail::fail;
+using mcgmil_detail::hip_fail;
+using mcgmil::bf16x8;
+using mcgmil::f32x4;
+
+constexpr int kThreads = 256;
+constexpr int kMaxC = 2048;           // channel groups of 8 <= threads of a workgroup
+constexpr int kMaxParts = 1024;       // statistics workgroups
+constexpr long long kBytesPerPart = 64 << 10;   // at least this much input per statistics workgroup
+constexpr int kFinCh = 8;             // finalize: channels per workgroup
+constexpr int kFinLanes = kThreads / kFinCh;    // finalize: lanes per channel
+
+__device__ __forceinline__ void load8(const __bf16* p, float (&v)[8]) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xFFFF0000u);
+    v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xFFFF0000u);
+    v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xFFFF0000u);
+    v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xFFFF0000u);
+}
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+__device__ __forceinline__ void store8(__bf16* p, const float (&v)[8]) {
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[j];             // round to nearest even
+    *reinterpret_cast<bf16x8*>(p) = o;
+}
+__device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
+    *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+
+// Workgroup b sums rows [b * rpp, (b + 1) * rpp). Thread (rp, cg): channels 8*cg .. 8*cg+7 of
+// rows r0 + rp, r0 + rp + RP, ... with RP = 256 / (C / 8) row lanes.
+template <typename E>
+__global__ __launch_bounds__(kThreads) void bn_partial_kernel(const E* __restrict__ x, long long rows,
+                                                              int C, long long rpp,
+                                                              float* __restrict__ part) {
+    __shared__ float red[2][kThreads * 8];
+    const int tid = threadIdx.x, CG = C >> 3, RP = kThreads / CG;
+    const int cg = tid % CG, rp = tid / CG;
+    const long long r0 = (long long)blockIdx.x * rpp;
+    const long long r1 = r0 + rpp < rows ? r0 + rpp : rows;
+    float s[8], ss[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = ss[j] = 0.f;
+    if (rp < RP) {
+        load8(x + cg * 8, sh);                       // shift: row 0
+        long long r = r0 + rp;
+        // two rows in flight per iteration (independent loads)
+        for (; r + RP < r1; r += 2 * RP) {
+            float v[8], w[8];
+            load8(x + r * C + cg * 8, v);
+            load8(x + (r + RP) * C + cg * 8, w);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float d = v[j] - sh[j], e = w[j] - sh[j];
+                s[j] += d + e;
+                ss[j] = fmaf(d, d, fmaf(e, e, ss[j]));
+            }
+        }
+        if (r < r1) {
+            float v[8];
+            load8(x + r * C + cg * 8, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float d = v[j] - sh[j];
+                s[j] += d;
+                ss[j] = fmaf(d, d, ss[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            red[0][rp * C + cg * 8 + j] = s[j];
+            red[1][rp * C + cg * 8 + j] = ss[j];
+        }
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += kThreads) {
+        float S = 0.f, SS = 0.f;
+        for (int k = 0; k < RP; ++k) {
+            S += red[0][k * C + c];
+            SS += red[1][k * C + c];
+        }
+        part[((size_t)blockIdx.x * 2) * C + c] = S;
+        part[((size_t)blockIdx.x * 2 + 1) * C + c] = SS;
+    }
+}
+
+// One workgroup per 8 channels, 32 lanes per channel each summing every 32nd partial in fp64;
+// the 32 lane sums are combined in lane order (deterministic for a given partial count).
+template <typename E>
+__global__ __launch_bounds__(kThreads) void bn_finalize_kernel(const float* __restrict__ part, int parts,
+                                                               long long rows, int C, const E* __restrict__ x,
+                                                               const float* gamma, const float* beta,
+                                                               const float* rmean, const float* rvar,
+                                                               double eps, float* __restrict__ ab,
+                                                               float* bmean, float* binvstd) {
+    __shared__ double red[2][kThreads];
+    const int tid = threadIdx.x, lane = tid / kFinCh, cl = tid % kFinCh;
+    const int c = blockIdx.x * kFinCh + cl;
+    double S = 0.0, SS = 0.0;
+    if (!rmean && c < C) {
+        for (int b = lane; b < parts; b += kFinLanes) {
+            S += (double)part[((size_t)b * 2) * C + c];
+            SS += (double)part[((size_t)b * 2 + 1) * C + c];
+        }
+    }
+    red[0][tid] = S;
+    red[1][tid] = SS;
+    __syncthreads();
+    if (lane != 0 || c >= C) return;
+    double mean, var;
+    if (rmean) {
+        mean = rmean[c];
+        var = rvar[c];
+    } else {
+        S = SS = 0.0;
+        for (int k = 0; k < kFinLanes; ++k) {
+            S += red[0][k * kFinCh + cl];
+            SS += red[1][k * kFinCh + cl];
+        }
+        float sh[8];
+        load8(x + (c & ~7), sh);
+        const double m = S / (double)rows;
+        var = SS / (double)rows - m * m;
+        if (var < 0.0) var = 0.0;
+        mean = (double)sh[c & 7] + m;
+    }
+    const double inv = 1.0 / sqrt(var + eps);
+    const double g = gamma ? (double)gamma[c] : 1.0, bt = beta ? (double)beta[c] : 0.0;
+    ab[c] = (float)(g * inv);
+    ab[C + c] = (float)(bt - mean * g * inv);
+    if (bmean) bmean[c] = (float)mean;
+    if (binvstd) binvstd[c] = (float)inv;
+}
+
+// Grid-stride over 8-channel vectors; the total thread count is a multiple of C/8, so every
+// thread keeps one channel group. Two vectors in flight per iteration.
+template <typename E, bool RELU, bool RES>
+__global__ __launch_bounds__(kThreads) void bn_apply_kernel(const E* x, const E* res, E* y, long long nvec,
+                                                            int C, const float* __restrict__ ab) {
+    const int CG = C >> 3;
+    const long long stride = (long long)gridDim.x * kThreads;
+    const long long i0 = (long long)blockIdx.x * kThreads + threadIdx.x;
+    const int cg = (int)(i0 % CG);
+    float a[8], b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        a[j] = ab[cg * 8 + j];
+        b[j] = ab[C + cg * 8 + j];
+    }
+    auto one = [&](long long i, const float (&v)[8], const float (&r)[8]) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float t = fmaf(v[j], a[j], b[j]);
+            if (RES) t += r[j];
+            o[j] = RELU ? fmaxf(t, 0.f) : t;
+        }
+        store8(y + i * 8, o);
+    };
+    long long i = i0;
+    for (; i + stride < nvec; i += 2 * stride) {
+        float v[8], w[8], r[8], q[8];
+        load8(x + i * 8, v);
+        load8(x + (i + stride) * 8, w);
+        if (RES) {
+            load8(res + i * 8, r);
+            load8(res + (i + stride) * 8, q);
+        }
+        one(i, v, r);
+        one(i + stride, w, q);
+    }
+    if (i < nvec) {
+        float v[8], r[8];
+        load8(x + i * 8, v);
+        if (RES) load8(res + i * 8, r);
+        one(i, v, r);
+    }
+}
+
+// statistics workgroups: ~64 KB of input each (at least 4 row passes), at most 1024
+// Activation + k x k max-pool (stride s, pad p, -inf padding): thread per (output pixel,
+// 8-channel group); the window's inputs are re-read from L2 by the neighbouring outputs.
+template <typename E, bool RELU>
+__global__ __launch_bounds__(kThreads) void bn_pool_kernel(const E* __restrict__ x, E* __restrict__ y, int H,
+                                                           int W, int Ho, int Wo, int k, int st, int pd,
+                                                           long long nvec, int C, const float* __restrict__ ab) {
+    const int CG = C >> 3;
+    const long long stride = (long long)gridDim.x * kThreads;
+    const long long i0 = (long long)blockIdx.x * kThreads + threadIdx.x;
+    const int cg = (int)(i0 % CG);
+    float a[8], b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        a[j] = ab[cg * 8 + j];
+        b[j] = ab[C + cg * 8 + j];
+    }
+    for (long long i = i0; i < nvec; i += stride) {
+        const long long pix = i / CG;
+        const int ow = (int)(pix % Wo);
+        const long long t = pix / Wo;
+        const int oh = (int)(t % Ho);
+        const long long n = t / Ho;
+        float m[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+        const int h0 = oh * st - pd, w0 = ow * st - pd;
+        for (int kh = 0; kh < k; ++kh) {
+            const int ih = h0 + kh;
+            if (ih < 0 || ih >= H) continue;
+            const E* row = x + ((n * H + ih) * (long long)W) * C + cg * 8;
+            for (int kw = 0; kw < k; ++kw) {
+                const int iw = w0 + kw;
+                if (iw < 0 || iw >= W) continue;
+                float v[8];
+                load8(row + (long long)iw * C, v);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fmaf(v[j], a[j], b[j]));
+            }
+        }
+        if (RELU) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], 0.f);
+        }
+        store8(y + i * 8, m);
+    }
+}
+
+int pooled_dim(int size, const mcgmil_bn_args* a) {
+    return (size + 2 * a->pool_pad - a->pool_kernel) / a->pool_stride + 1;
+}
+
+int parts_for(const mcgmil_bn_args* a) {
+    const long long esz = a->dtype == MCGMIL_BF16 ? 2 : 4;
+    const long long row_bytes = (long long)a->channels * esz;
+    const long long RP = kThreads / (a->channels / 8);
+    long long rpp = kBytesPerPart / row_bytes;
+    if (rpp < 4 * RP) rpp = 4 * RP;
+    const long long p = (a->rows + rpp - 1) / rpp;
+    return (int)(p < kMaxParts ? (p < 1 ? 1 : p) : kMaxParts);
+}
+
+size_t ws_bytes(const mcgmil_bn_args* a) {
+    const size_t f = (size_t)2 * a->channels * (1 + (size_t)parts_for(a));
+    return (f * sizeof(float) + 255) & ~(size_t)255;
+}
+
+int validate(const mcgmil_bn_args* a) {
+    if (!a) return fail(MCGMIL_E_INVALID, "mcgmil_bn_args is NULL");
+    if (a->rows < 1) return fail(MCGMIL_E_INVALID, "rows must be >= 1");
+    if (a->channels < 8 || a->channels % 8 || a->channels > kMaxC)
+        return fail(MCGMIL_E_UNSUPPORTED, "channels must be a multiple of 8 in [8, 2048], got " +
+                                              std::to_string(a->channels));
+    if (a->dtype != MCGMIL_BF16 && a->dtype != MCGMIL_F32)
+        return fail(MCGMIL_E_INVALID, "dtype must be MCGMIL_BF16 or MCGMIL_F32");
+    if (!a->x || !a->y) return fail(MCGMIL_E_INVALID, "x and y are required");
+    if (((uintptr_t)a->x | (uintptr_t)a->y | (uintptr_t)a->residual) & 15)
+        return fail(MCGMIL_E_ALIGN, "x, y and residual must be 16-byte aligned");
+    if ((a->running_mean == nullptr) != (a->running_var == nullptr))
+        return fail(MCGMIL_E_INVALID, "running_mean and running_var go together");
+    if (!(a->eps >= 0.0)) return fail(MCGMIL_E_INVALID, "eps must be >= 0");
+    if (a->relu != 0 && a->relu != 1) return fail(MCGMIL_E_INVALID, "relu must be 0 or 1");
+    if (a->pool_kernel < 0) return fail(MCGMIL_E_INVALID, "pool_kernel must be >= 0");
+    if (a->pool_kernel > 0) {
+        if (a->batch < 1 || a->height < 1 || a->width < 1 ||
+            (long long)a->batch * a->height * a->width != a->rows)
+            return fail(MCGMIL_E_INVALID, "pooling needs batch * height * width == rows");
+        if (a->pool_stride < 1 || a->pool_pad < 0 || 2 * a->pool_pad > a->pool_kernel)
+            return fail(MCGMIL_E_INVALID, "pooling needs stride >= 1 and 0 <= pad <= kernel / 2");
+        if (pooled_dim(a->height, a) < 1 || pooled_dim(a->width, a) < 1)
+            return fail(MCGMIL_E_INVALID, "pooling window larger than the padded input");
+        if (a->residual) return fail(MCGMIL_E_UNSUPPORTED, "no residual add with pooling");
+        if (a->x == a->y) return fail(MCGMIL_E_INVALID, "pooling cannot run in place");
+    }
+    return MCGMIL_OK;
+}
+
+template <typename E, bool RELU, bool RES>
+void launch_apply(const mcgmil_bn_args* a, const float* ab, hipStream_t s) {
+    const long long nvec = a->rows * (a->channels / 8);
+    const int CG = a->channels / 8;
+    // blocks: a multiple of CG / gcd(CG, 256) so that every thread keeps its channel group
+    const int unit = CG / std::gcd(CG, kThreads);
+    long long want = (nvec + 2LL * kThreads - 1) / (2LL * kThreads);
+    if (want > 4096) want = 4096;
+    long long blocks = (want + unit - 1) / unit * unit;
+    hipLaunchKernelGGL((bn_apply_kernel<E, RELU, RES>), dim3((unsigned)blocks), dim3(kThreads), 0, s,
+                       static_cast<const E*>(a->x), static_cast<const E*>(a->residual),
+                       static_cast<E*>(a->y), nvec, a->channels, ab);
+}
+
+template <typename E>
+int run(const mcgmil_bn_args* a, hipStream_t s) {
+    const int C = a->channels;
+    float* ws = static_cast<float*>(a->workspace);
+    float* ab = ws;                      // [2][C]
+    float* part = ws + 2 * C;            // [parts][2][C]
+    const E* x = static_cast<const E*>(a->x);
+    int parts = 0;
+    if (!a->running_mean) {
+        parts = parts_for(a);
+        const long long rpp = (a->rows + parts - 1) / parts;
+        hipLaunchKernelGGL(bn_partial_kernel<E>, dim3(parts), dim3(kThreads), 0, s, x, a->rows, C, rpp, part);
+    }
+    hipLaunchKernelGGL(bn_finalize_kernel<E>, dim3((C + kFinCh - 1) / kFinCh), dim3(kThreads), 0, s, part, parts, a->rows,
+                       C, x, a->gamma, a->beta, a->running_mean, a->running_var, a->eps, ab,
+                       a->batch_mean, a->batch_invstd);
+    if (a->pool_kernel > 0) {
+        const int Ho = pooled_dim(a->height, a), Wo = pooled_dim(a->width, a);
+        const long long nvec = (long long)a->batch * Ho * Wo * (C / 8);
+        const int unit = (C / 8) / std::gcd(C / 8, kThreads);
+        long long want = (nvec + kThreads - 1) / kThreads;
+        if (want > 8192) want = 8192;
+        const long long blocks = (want + unit - 1) / unit * unit;
+        auto k = a->relu ? bn_pool_kernel<E, true> : bn_pool_kernel<E, false>;
+        hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kThreads), 0, s, x, static_cast<E*>(a->y),
+                           a->height, a->width, Ho, Wo, a->pool_kernel, a->pool_stride, a->pool_pad,
+                           nvec, C, ab);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "batchnorm pool launch");
+    }
+    const bool res = a->residual != nullptr;
+    if (a->relu) {
+        if (res) launch_apply<E, true, true>(a, ab, s);
+        else launch_apply<E, true, false>(a, ab, s);
+    } else {
+        if (res) launch_apply<E, false, true>(a, ab, s);
+        else launch_apply<E, false, false>(a, ab, s);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "batchnorm launch");
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t mcgmil_bn_args_size(void) { return sizeof(mcgmil_bn_args); }
+
+int mcgmil_bn_workspace_size(const mcgmil_bn_args* a, size_t* bytes) {
+    if (int rc = validate(a)) return rc;
+    if (!bytes) return fail(MCGMIL_E_INVALID, "bytes is NULL");
+    *bytes = ws_bytes(a);
+    return MCGMIL_OK;
+}
+
+int mcgmil_batchnorm_act(const mcgmil_bn_args* a, void* stream) {
+    if (int rc = validate(a)) return rc;
+    if (!a->workspace || a->workspace_bytes < ws_bytes(a) || ((uintptr_t)a->workspace & 255))
+        return fail(MCGMIL_E_WORKSPACE, "workspace missing, misaligned or smaller than "
+                                        "mcgmil_bn_workspace_size()");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    return a->dtype == MCGMIL_BF16 ? run<__bf16>(a, s) : run<float>(a, s);
+}
+
+}  // extern "C"

@@ -11,8 +11,8 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(os.path.dirname(ROOT), "include")
 LIB = os.path.join(PKG, "libmcgmil.so")
-SOURCES = ["mcgmil.hip", "mcgmil_image.hip"]
-DEPS = ["mcgmil.hip", "mcgmil_image.hip", "mcgmil_kernels.h", "mcgmil_device.h",
+SOURCES = ["mcgmil.hip", "mcgmil_image.hip", "mcgmil_bn.hip"]
+DEPS = ["mcgmil.hip", "mcgmil_image.hip", "mcgmil_bn.hip", "mcgmil_kernels.h", "mcgmil_device.h",
         "mcgmil_error.h", "mcgmil_gate_pp.h"]
 ARCH = os.environ.get("MCGMIL_OFFLOAD_ARCH", "gfx950")
 # No packed-fp32 VALU (v_pk_fma/mul/add_f32): with ROCm 7.2's compiler a packed write into the
@@ -29,7 +29,7 @@ def _stale(out: str = LIB) -> bool:
     if os.path.getmtime(os.path.abspath(__file__)) > t:      # build flags changed
         return True
     deps = [os.path.join(CSRC, d) for d in DEPS] + \
-        [os.path.join(INCLUDE, h) for h in ("mcgmil.h", "mcgmil_image.h")]
+        [os.path.join(INCLUDE, h) for h in ("mcgmil.h", "mcgmil_image.h", "mcgmil_features.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 

@@ -26,6 +26,8 @@ EXPORTED = (
     # include/mcgmil_image.h
     "mcgmil_image_args_size", "mcgmil_tile_grid", "mcgmil_image_workspace_size",
     "mcgmil_image_to_bag", "mcgmil_attention_maps", "mcgmil_reconstruct_image",
+    # include/mcgmil_features.h
+    "mcgmil_bn_args_size", "mcgmil_bn_workspace_size", "mcgmil_batchnorm_act",
 )
 
 _vp = ctypes.c_void_p
@@ -65,6 +67,20 @@ class ImageArgs(ctypes.Structure):
         ("T", ctypes.c_int32), ("C", ctypes.c_int32), ("k", ctypes.c_int32),
         ("attention", _vp), ("map_tile_ids", _vp), ("maps", _vp), ("map_mean", _vp),
         ("map_std", _vp), ("patches", _vp), ("image_out", _vp),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
+class BnArgs(ctypes.Structure):
+    """Mirror of struct mcgmil_bn_args (include/mcgmil_features.h)."""
+    _fields_ = [
+        ("rows", ctypes.c_int64), ("channels", ctypes.c_int32), ("dtype", ctypes.c_int32),
+        ("x", _vp), ("residual", _vp), ("y", _vp), ("gamma", _vp), ("beta", _vp),
+        ("running_mean", _vp), ("running_var", _vp), ("eps", ctypes.c_double),
+        ("relu", ctypes.c_int32), ("batch", ctypes.c_int32), ("height", ctypes.c_int32),
+        ("width", ctypes.c_int32), ("pool_kernel", ctypes.c_int32), ("pool_stride", ctypes.c_int32),
+        ("pool_pad", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("batch_mean", _vp), ("batch_invstd", _vp),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
     ]
 
@@ -119,6 +135,15 @@ def load():
         f = getattr(L, name)
         f.argtypes = [pi, _vp]
         f.restype = ctypes.c_int
+    pb = ctypes.POINTER(BnArgs)
+    L.mcgmil_bn_args_size.restype = ctypes.c_size_t
+    L.mcgmil_bn_workspace_size.argtypes = [pb, ctypes.POINTER(ctypes.c_size_t)]
+    L.mcgmil_bn_workspace_size.restype = ctypes.c_int
+    L.mcgmil_batchnorm_act.argtypes = [pb, _vp]
+    L.mcgmil_batchnorm_act.restype = ctypes.c_int
+    if L.mcgmil_bn_args_size() != ctypes.sizeof(BnArgs):
+        raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_bn_args)={L.mcgmil_bn_args_size()} "
+                          f"but the ctypes mirror is {ctypes.sizeof(BnArgs)} bytes")
     if L.mcgmil_image_args_size() != ctypes.sizeof(ImageArgs):
         raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_image_args)={L.mcgmil_image_args_size()} "
                           f"but the ctypes mirror is {ctypes.sizeof(ImageArgs)} bytes")

@@ -9,11 +9,17 @@ Identity (model.py:179) and, in infer.py, forces every BatchNorm to batch statis
 
 ImageNet weights cannot be downloaded offline: `pretrained=True` builds the same architecture
 with random initialisation and warns (load a checkpoint to get trained weights).
+
+Every `relu?(bn(conv(x)) [+ identity])` of the blocks goes through `features.bn_act`: on the GPU
+with channels-last activations it is one fused HIP BatchNorm(+add)(+ReLU) (include/
+mcgmil_features.h); elsewhere (CPU, autograd) it is the torch layers.
 """
 import warnings
 
 import torch
 import torch.nn as nn
+
+from .features import bn_act
 
 
 class Identity(nn.Module):
@@ -29,6 +35,15 @@ def deactivate_batchnorm(net):
         net.track_running_stats = False
         net.running_mean = None
         net.running_var = None
+
+
+def _identity(down, x):
+    """The block's shortcut: x, or downsample = Sequential(conv1x1, BatchNorm2d) (no ReLU)."""
+    if down is None:
+        return x
+    if isinstance(down, nn.Sequential) and len(down) == 2 and isinstance(down[1], nn.BatchNorm2d):
+        return bn_act(down[1], down[0](x), False)
+    return down(x)
 
 
 def _conv3x3(i, o, stride=1):
@@ -48,10 +63,9 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.bn2(self.conv2(y))
-        return self.relu(y + idt)
+        idt = _identity(self.downsample, x)
+        y = bn_act(self.bn1, self.conv1(x), True)
+        return bn_act(self.bn2, self.conv2(y), True, idt)
 
 
 class Bottleneck(nn.Module):
@@ -69,11 +83,10 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.relu(self.bn2(self.conv2(y)))
-        y = self.bn3(self.conv3(y))
-        return self.relu(y + idt)
+        idt = _identity(self.downsample, x)
+        y = bn_act(self.bn1, self.conv1(x), True)
+        y = bn_act(self.bn2, self.conv2(y), True)
+        return bn_act(self.bn3, self.conv3(y), True, idt)
 
 
 class ResNet(nn.Module):
@@ -105,7 +118,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = bn_act(self.bn1, self.conv1(x), True, pool=self.maxpool)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

@@ -8,7 +8,7 @@ import pytest
 
 from conftest import REPO
 
-HEADERS = [os.path.join(REPO, "include", h) for h in ("mcgmil.h", "mcgmil_image.h")]
+HEADERS = [os.path.join(REPO, "include", h) for h in ("mcgmil.h", "mcgmil_image.h", "mcgmil_features.h")]
 
 
 def declared_functions():
@@ -45,6 +45,7 @@ def test_args_struct_matches_binding(hip_lib):
     assert hip_lib.mcgmil_abi_version() == 1
     assert hip_lib.mcgmil_args_size() == ctypes.sizeof(_lib.Args)
     assert hip_lib.mcgmil_image_args_size() == ctypes.sizeof(_lib.ImageArgs)
+    assert hip_lib.mcgmil_bn_args_size() == ctypes.sizeof(_lib.BnArgs)
 
 
 def _args(**kw):
@@ -103,3 +104,33 @@ def test_gate_rejects_misaligned_H(hip_lib):
     assert hip_lib.mcgmil_gate_scores(ctypes.byref(a), None) == -3
     a.H, a.ldh = ctypes.c_void_p(0x3000), 509
     assert hip_lib.mcgmil_gate_scores(ctypes.byref(a), None) == -1  # ldh < L
+
+
+def _bn(**kw):
+    from mcgmil import _lib
+    a = _lib.BnArgs()
+    a.rows, a.channels, a.dtype, a.eps = 4096, 64, _lib.MCGMIL_BF16, 1e-5
+    a.x = a.y = ctypes.c_void_p(0x10000)
+    for k, v in kw.items():
+        setattr(a, k, v)
+    return a
+
+
+def test_bn_workspace_size_and_validation(hip_lib):
+    """mcgmil_features.h: the workspace query and the argument checks (no launches)."""
+    from mcgmil import _lib
+    n = ctypes.c_size_t()
+    assert hip_lib.mcgmil_bn_workspace_size(ctypes.byref(_bn()), ctypes.byref(n)) == 0
+    assert n.value >= 2 * 64 * 4 * 5 and n.value % 256 == 0       # ab + 4 partial workgroups
+    bad = {"channels": 12, "rows": 0, "dtype": 7, "relu": 2, "eps": -1.0}
+    for k, v in bad.items():
+        rc = hip_lib.mcgmil_bn_workspace_size(ctypes.byref(_bn(**{k: v})), ctypes.byref(n))
+        assert rc in (-1, -2), (k, rc)
+    assert hip_lib.mcgmil_bn_workspace_size(ctypes.byref(_bn(channels=4096)), ctypes.byref(n)) == -2
+    assert hip_lib.mcgmil_bn_workspace_size(ctypes.byref(_bn(x=ctypes.c_void_p(0x10008))),
+                                            ctypes.byref(n)) == -3
+    rc = hip_lib.mcgmil_bn_workspace_size(ctypes.byref(_bn(running_mean=ctypes.c_void_p(0x2000))),
+                                          ctypes.byref(n))
+    assert rc == -1 and b"running_var" in hip_lib.mcgmil_last_error()
+    # a missing workspace is refused before anything is launched
+    assert hip_lib.mcgmil_batchnorm_act(ctypes.byref(_bn()), None) == -4
