@@ -29,7 +29,7 @@ run() {  # name seconds cmd...
 for s in $STEPS; do
     case $s in
         smoke) run smoke 420 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
-        tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+        tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
         bench) run bench 600 python bench.py ;;
         imgtests) run pytest_gpu_image 600 python -m pytest tests/test_gpu_image.py -m gpu -q -rf ;;
         imgprobe) run probe_image 300 python scripts/probe_image.py ;;
