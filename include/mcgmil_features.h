@@ -10,6 +10,11 @@
  *                          running stats None -> every forward normalises with the statistics
  *                          of the bag itself)
  *
+ *   mcgmil_conv2d          torch.nn.Conv2d.forward (bias=False, groups=1, dilation=1) of the
+ *                          backbone's 3x3 / 1x1 convolutions (torchvision BasicBlock /
+ *                          Bottleneck, model.py:166-177) under torch.autocast bf16, applied to
+ *                          every instance of the bag at infer.py:191 -> model.py:275-277
+ *
  * Layout: activations are channels-last (NHWC), i.e. a row-major [rows = N*H*W, C] matrix;
  * C a multiple of 8, rows >= 1, x / residual / y 16-byte aligned.
  *
@@ -65,6 +70,27 @@ typedef struct mcgmil_bn_args {
 } mcgmil_bn_args;
 
 size_t mcgmil_bn_args_size(void);   /* sizeof(mcgmil_bn_args), for binding checks */
+
+/* Convolution y = conv2d(x, w, stride, pad) of channels-last bf16 activations as an implicit GEMM
+ * on the matrix cores (fp32 accumulation, one rounding to bf16 -- torch.autocast's arithmetic up
+ * to the summation order). x is [batch, height, width, in_channels], y is [batch, OH, OW,
+ * out_channels] with OH = (height + 2 pad - kernel_h) / stride + 1 (likewise OW), both NHWC;
+ * w is the packed weight [out_channels, kernel_h, kernel_w, in_channels] bf16 made by
+ * mcgmil_pack_conv_weights from the torch layout [out, in, kh, kw] (fp32 or bf16). Zero padding.
+ * in/out channels multiples of 64; kernel 1..7; x < 2 GiB; pointers 16-byte aligned. */
+typedef struct mcgmil_conv_args {
+    int32_t batch, height, width, in_channels;
+    int32_t out_channels, kernel_h, kernel_w, stride, pad;
+    int32_t reserved;
+    const void* x;              /* bf16 [batch, height, width, in_channels] */
+    const void* w;              /* packed bf16 [out_channels, kernel_h, kernel_w, in_channels] */
+    void* y;                    /* bf16 [batch, OH, OW, out_channels] */
+} mcgmil_conv_args;
+
+size_t mcgmil_conv_args_size(void);
+int mcgmil_pack_conv_weights(const mcgmil_conv_args* a, const void* weight, int32_t weight_dtype,
+                             void* packed, void* stream);
+int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream);
 int mcgmil_bn_workspace_size(const mcgmil_bn_args* a, size_t* bytes);
 int mcgmil_batchnorm_act(const mcgmil_bn_args* a, void* stream);
 

@@ -28,6 +28,7 @@ EXPORTED = (
     "mcgmil_image_to_bag", "mcgmil_attention_maps", "mcgmil_reconstruct_image",
     # include/mcgmil_features.h
     "mcgmil_bn_args_size", "mcgmil_bn_workspace_size", "mcgmil_batchnorm_act",
+    "mcgmil_conv_args_size", "mcgmil_pack_conv_weights", "mcgmil_conv2d",
 )
 
 _vp = ctypes.c_void_p
@@ -68,6 +69,17 @@ class ImageArgs(ctypes.Structure):
         ("attention", _vp), ("map_tile_ids", _vp), ("maps", _vp), ("map_mean", _vp),
         ("map_std", _vp), ("patches", _vp), ("image_out", _vp),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
+class ConvArgs(ctypes.Structure):
+    """Mirror of struct mcgmil_conv_args (include/mcgmil_features.h)."""
+    _fields_ = [
+        ("batch", ctypes.c_int32), ("height", ctypes.c_int32), ("width", ctypes.c_int32),
+        ("in_channels", ctypes.c_int32), ("out_channels", ctypes.c_int32),
+        ("kernel_h", ctypes.c_int32), ("kernel_w", ctypes.c_int32), ("stride", ctypes.c_int32),
+        ("pad", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("x", _vp), ("w", _vp), ("y", _vp),
     ]
 
 
@@ -141,6 +153,15 @@ def load():
     L.mcgmil_bn_workspace_size.restype = ctypes.c_int
     L.mcgmil_batchnorm_act.argtypes = [pb, _vp]
     L.mcgmil_batchnorm_act.restype = ctypes.c_int
+    pc = ctypes.POINTER(ConvArgs)
+    L.mcgmil_conv_args_size.restype = ctypes.c_size_t
+    L.mcgmil_pack_conv_weights.argtypes = [pc, _vp, ctypes.c_int32, _vp, _vp]
+    L.mcgmil_pack_conv_weights.restype = ctypes.c_int
+    L.mcgmil_conv2d.argtypes = [pc, _vp]
+    L.mcgmil_conv2d.restype = ctypes.c_int
+    if L.mcgmil_conv_args_size() != ctypes.sizeof(ConvArgs):
+        raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_conv_args)={L.mcgmil_conv_args_size()} "
+                          f"but the ctypes mirror is {ctypes.sizeof(ConvArgs)} bytes")
     if L.mcgmil_bn_args_size() != ctypes.sizeof(BnArgs):
         raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_bn_args)={L.mcgmil_bn_args_size()} "
                           f"but the ctypes mirror is {ctypes.sizeof(BnArgs)} bytes")

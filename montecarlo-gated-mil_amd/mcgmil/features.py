@@ -1,5 +1,5 @@
-"""Fused BatchNorm + residual add + ReLU of the channels-last backbone on the GPU
-(include/mcgmil_features.h, mcgmil_batchnorm_act).
+"""The channels-last backbone's layers on the GPU (include/mcgmil_features.h): fused BatchNorm +
+residual add + ReLU (mcgmil_batchnorm_act) and the implicit-GEMM convolution (mcgmil_conv2d).
 
 The reference runs its ResNet's BatchNorm2d layers on the statistics of the bag itself
 (infer.py:105-109 deactivate_batchnorm: running stats None, so torch.nn.functional.batch_norm
@@ -13,6 +13,13 @@ normalised with them.
 activation with C % 8 == 0 and C <= 2048, no autograd, and no running-statistics update pending
 (a BN in training mode that tracks running stats keeps the torch path, which updates them).
 MCGMIL_FUSED_BN=0 switches the backbone back to the torch layers (A/B timing and parity tests).
+
+`conv2d` runs a 3x3 / 1x1 torch.nn.Conv2d of the blocks (bias-free, groups 1, dilation 1, zero
+padding, 64k input and output channels) on a channels-last bf16 activation as one MFMA
+implicit-GEMM kernel -- the arithmetic of torch.autocast's bf16 convolution (bf16 operands, fp32
+accumulation, one rounding) without MIOpen's per-convolution output fill. `conv_fusable` says when
+it applies; the stem (3 input channels) and everything else keep torch's convolution.
+MCGMIL_NATIVE_CONV=0 switches it off.
 """
 import ctypes
 import os
@@ -46,6 +53,96 @@ def fusable(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor
     if bn.training and bn.track_running_stats and bn.running_mean is not None:
         return False                       # torch would update the running statistics
     return True
+
+
+def conv_enabled() -> bool:
+    return os.environ.get("MCGMIL_NATIVE_CONV", "1") != "0"
+
+
+def _square(v):
+    return v if isinstance(v, int) else (v[0] if len(set(v)) == 1 else None)
+
+
+def conv_fusable(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """A CUDA channels-last activation that torch would convolve in bf16 (bf16 input, or autocast
+    to bf16), with a convolution the kernel implements, and no autograd."""
+    if not (conv_enabled() and isinstance(conv, nn.Conv2d) and x.is_cuda and x.dim() == 4):
+        return False
+    if conv.groups != 1 or conv.bias is not None or conv.padding_mode != "zeros":
+        return False
+    if _square(conv.dilation) != 1 or _square(conv.stride) is None or \
+            not isinstance(conv.padding, tuple) or _square(conv.padding) is None:
+        return False
+    kh, kw = conv.kernel_size
+    if not (1 <= kh <= 7 and 1 <= kw <= 7):
+        return False
+    if conv.in_channels % 64 or conv.out_channels % 64 or x.shape[1] != conv.in_channels:
+        return False
+    bf16 = x.dtype == torch.bfloat16 and (
+        conv.weight.dtype == torch.bfloat16 or
+        (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16))
+    if not bf16 or not x.is_contiguous(memory_format=torch.channels_last):
+        return False
+    if torch.is_grad_enabled() and (x.requires_grad or conv.weight.requires_grad):
+        return False
+    return x.numel() * 2 < 2 ** 31
+
+
+def _conv_args(conv: nn.Conv2d, x: torch.Tensor):
+    a = _lib.ConvArgs()
+    a.batch, _, a.height, a.width = x.shape
+    a.in_channels, a.out_channels = conv.in_channels, conv.out_channels
+    a.kernel_h, a.kernel_w = conv.kernel_size
+    a.stride, a.pad = _square(conv.stride), _square(conv.padding)
+    return a
+
+
+def packed_conv_weight(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """The weight as bf16 [out, kh, kw, in] (torch's autocast cast, then channels-last), cached on
+    the module until the weight changes."""
+    w = conv.weight.detach()
+    key = (w.data_ptr(), w._version, w.dtype, x.device)
+    cached = getattr(conv, "_mcgmil_packed", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    L = _lib.load()
+    if w.device != x.device or w.dtype not in (torch.float32, torch.bfloat16):
+        w = w.to(device=x.device, dtype=torch.float32)
+    w = w.contiguous()
+    packed = torch.empty(w.numel(), dtype=torch.bfloat16, device=x.device)
+    a = _conv_args(conv, x)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    _lib.check(L.mcgmil_pack_conv_weights(ctypes.byref(a), ctypes.c_void_p(w.data_ptr()),
+                                          _DT[w.dtype], ctypes.c_void_p(packed.data_ptr()), stream),
+               "mcgmil_pack_conv_weights")
+    conv._mcgmil_packed = (key, packed)
+    return packed
+
+
+def conv2d(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """conv(x) for a channels-last bf16 activation (see conv_fusable) on the MFMA kernel; returns a
+    channels-last bf16 tensor."""
+    if not conv_fusable(conv, x):
+        raise ValueError("conv2d needs a CUDA channels-last bf16 activation, a bias-free groups=1 "
+                         "convolution with 64k channels and no autograd (see conv_fusable)")
+    L = _lib.load()
+    a = _conv_args(conv, x)
+    oh = (a.height + 2 * a.pad - a.kernel_h) // a.stride + 1
+    ow = (a.width + 2 * a.pad - a.kernel_w) // a.stride + 1
+    y = torch.empty((a.batch, a.out_channels, oh, ow), dtype=torch.bfloat16, device=x.device,
+                    memory_format=torch.channels_last)
+    w = packed_conv_weight(conv, x)
+    a.x, a.w, a.y = (ctypes.c_void_p(t.data_ptr()) for t in (x, w, y))
+    stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    _lib.check(L.mcgmil_conv2d(ctypes.byref(a), stream), "mcgmil_conv2d")
+    return y
+
+
+def run_conv(layer: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """The backbone's convolution: the MFMA kernel when `conv_fusable`, else the torch layer."""
+    if isinstance(layer, nn.Conv2d) and conv_fusable(layer, x):
+        return conv2d(layer, x)
+    return layer(x)
 
 
 def _f32(t: Optional[torch.Tensor], dev) -> Optional[torch.Tensor]:

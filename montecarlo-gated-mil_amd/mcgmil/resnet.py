@@ -10,16 +10,17 @@ Identity (model.py:179) and, in infer.py, forces every BatchNorm to batch statis
 ImageNet weights cannot be downloaded offline: `pretrained=True` builds the same architecture
 with random initialisation and warns (load a checkpoint to get trained weights).
 
-Every `relu?(bn(conv(x)) [+ identity])` of the blocks goes through `features.bn_act`: on the GPU
-with channels-last activations it is one fused HIP BatchNorm(+add)(+ReLU) (include/
-mcgmil_features.h); elsewhere (CPU, autograd) it is the torch layers.
+Every `relu?(bn(conv(x)) [+ identity])` of the blocks goes through `features.run_conv` and
+`features.bn_act`: on the GPU with channels-last bf16 activations they are the MFMA
+implicit-GEMM convolution and one fused HIP BatchNorm(+add)(+ReLU) (include/mcgmil_features.h);
+elsewhere (CPU, autograd, fp32) they are the torch layers.
 """
 import warnings
 
 import torch
 import torch.nn as nn
 
-from .features import bn_act
+from .features import bn_act, run_conv
 
 
 class Identity(nn.Module):
@@ -42,7 +43,7 @@ def _identity(down, x):
     if down is None:
         return x
     if isinstance(down, nn.Sequential) and len(down) == 2 and isinstance(down[1], nn.BatchNorm2d):
-        return bn_act(down[1], down[0](x), False)
+        return bn_act(down[1], run_conv(down[0], x), False)
     return down(x)
 
 
@@ -64,8 +65,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         idt = _identity(self.downsample, x)
-        y = bn_act(self.bn1, self.conv1(x), True)
-        return bn_act(self.bn2, self.conv2(y), True, idt)
+        y = bn_act(self.bn1, run_conv(self.conv1, x), True)
+        return bn_act(self.bn2, run_conv(self.conv2, y), True, idt)
 
 
 class Bottleneck(nn.Module):
@@ -84,9 +85,9 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         idt = _identity(self.downsample, x)
-        y = bn_act(self.bn1, self.conv1(x), True)
-        y = bn_act(self.bn2, self.conv2(y), True)
-        return bn_act(self.bn3, self.conv3(y), True, idt)
+        y = bn_act(self.bn1, run_conv(self.conv1, x), True)
+        y = bn_act(self.bn2, run_conv(self.conv2, y), True)
+        return bn_act(self.bn3, run_conv(self.conv3, y), True, idt)
 
 
 class ResNet(nn.Module):

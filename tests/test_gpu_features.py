@@ -140,6 +140,7 @@ def test_fusable_gates(cuda):
 def _backbone_features(cuda, fused, dtype):
     from mcgmil.resnet import build_backbone, deactivate_batchnorm, Identity
     os.environ["MCGMIL_FUSED_BN"] = "1" if fused else "0"
+    os.environ["MCGMIL_NATIVE_CONV"] = "1" if fused else "0"
     try:
         torch.manual_seed(0)
         net = build_backbone("r18", pretrained=False)
@@ -156,12 +157,14 @@ def _backbone_features(cuda, fused, dtype):
             return net(x)
     finally:
         os.environ.pop("MCGMIL_FUSED_BN", None)
+        os.environ.pop("MCGMIL_NATIVE_CONV", None)
 
 
 def test_backbone_fused_bn_matches_torch_layers(cuda):
     """fp32: the fused backbone equals the torch layers to 1e-4 nrel. bf16 autocast: both paths
-    drift from the fp32 features through 17 bf16 convolutions; the fused one (one rounding per
-    layer, fp64-combined statistics) must be no further from them than the torch layers are."""
+    drift from the fp32 features through 17 bf16 convolutions; the fused one (implicit-GEMM
+    convolutions, one rounding per BN layer, fp64-combined statistics) must be no further from
+    them than the torch layers are."""
     ref = _backbone_features(cuda, False, torch.float32)
     f32 = _backbone_features(cuda, True, torch.float32)
     nrel = lambda a, b: float((a - b).abs().max() / b.abs().max())  # noqa: E731
