@@ -143,7 +143,7 @@ def run(args, world, rank, dev, peak_tflops):
                    "stage_ms": stage_ms, "parallelism": f"one image per GPU per step, {world} GPU(s)"},
         "roofline": {"bound": "mfma", "achieved": feat_tflops, "peak": peak_tflops, "unit": "TFLOP/s",
                      "frac": feat_tflops / peak_tflops, "traffic": None,
-                     "kernel": "ResNet-18 feature extractor (MIOpen convolutions, the dominant stage)",
+                     "kernel": "ResNet-18 feature extractor (stem + implicit-GEMM convolutions + fused BN, the dominant stage)",
                      "algorithmic_tflop_per_launch": k * RESNET18_GFLOP / 1e3},
         "cpu_baseline": cpu,
     }

@@ -10,6 +10,10 @@
  *                          running stats None -> every forward normalises with the statistics
  *                          of the bag itself)
  *
+ *   mcgmil_stem_forward    the torchvision stem maxpool(relu(bn1(conv1(x)))) of the same
+ *                          backbone (ResNet.forward's first four layers), from the NCHW
+ *                          instances the image patcher writes
+ *
  *   mcgmil_conv2d          torch.nn.Conv2d.forward (bias=False, groups=1, dilation=1) of the
  *                          backbone's 3x3 / 1x1 convolutions (torchvision BasicBlock /
  *                          Bottleneck, model.py:166-177) under torch.autocast bf16, applied to
@@ -90,6 +94,45 @@ typedef struct mcgmil_conv_args {
 size_t mcgmil_conv_args_size(void);
 int mcgmil_pack_conv_weights(const mcgmil_conv_args* a, const void* weight, int32_t weight_dtype,
                              void* packed, void* stream);
+
+/* The ResNet stem pool(relu(bn1(conv1(x)))) in one call -- replaces torchvision ResNet.forward's
+ * first four layers (conv1 7x7/2 pad 3, bn1, relu, maxpool 3x3/2 pad 1; model.py:166-177 builds
+ * the backbone, infer.py:191 runs it on every instance of a bag) under torch.autocast bf16.
+ * x is the instance batch straight from mcgmil_image_to_bag: NCHW bf16 [batch, in_channels,
+ * height, width]; y is channels-last bf16 [batch, PH, PW, 64] (NHWC), PH/PW the pooled sizes
+ * (or OH/OW without pooling). The convolution is an implicit GEMM on the matrix cores (fp32
+ * accumulation, one rounding to bf16, as autocast's convolution); with batch statistics its
+ * epilogue also accumulates the per-channel sums that BatchNorm needs (around a per-channel
+ * shift taken from the convolution at one pixel), so the 64-channel activation is read once,
+ * by the pooling pass. BatchNorm / ReLU / pooling semantics are those of mcgmil_batchnorm_act.
+ * Supported: in_channels 1..4, out_channels 64, square kernel <= 8 (kernel + (pad & 1) <= 8),
+ * stride 2, width even, OW <= 125; otherwise MCGMIL_E_UNSUPPORTED (the caller keeps torch's
+ * layers). w is packed by mcgmil_pack_stem_weights from the torch layout [64, in, k, k]. */
+typedef struct mcgmil_stem_args {
+    int32_t batch, in_channels, height, width;
+    int32_t out_channels, kernel, stride, pad;
+    int32_t pool_kernel, pool_stride, pool_pad;   /* 0: no pooling */
+    int32_t relu;
+    double eps;
+    const void* x;              /* bf16 NCHW [batch, in_channels, height, width] */
+    const void* w;              /* packed bf16 weights (mcgmil_stem_packed_size bytes) */
+    const float* gamma;         /* [64] or NULL (1) */
+    const float* beta;          /* [64] or NULL (0) */
+    const float* running_mean;  /* [64]: running-statistics mode when both are given */
+    const float* running_var;
+    void* y;                    /* bf16 NHWC [batch, PH, PW, 64] */
+    float* batch_mean;          /* optional out [64] */
+    float* batch_invstd;        /* optional out [64] */
+    void* workspace;            /* >= mcgmil_stem_workspace_size() bytes, 256-byte aligned */
+    size_t workspace_bytes;
+} mcgmil_stem_args;
+
+size_t mcgmil_stem_args_size(void);
+int mcgmil_stem_packed_size(const mcgmil_stem_args* a, size_t* bytes);
+int mcgmil_pack_stem_weights(const mcgmil_stem_args* a, const void* weight, int32_t weight_dtype,
+                             void* packed, void* stream);
+int mcgmil_stem_workspace_size(const mcgmil_stem_args* a, size_t* bytes);
+int mcgmil_stem_forward(const mcgmil_stem_args* a, void* stream);
 int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream);
 int mcgmil_bn_workspace_size(const mcgmil_bn_args* a, size_t* bytes);
 int mcgmil_batchnorm_act(const mcgmil_bn_args* a, void* stream);

@@ -318,21 +318,14 @@ void launch_apply(const mcgmil_bn_args* a, const float* ab, hipStream_t s) {
                        static_cast<E*>(a->y), nvec, a->channels, ab);
 }
 
+// finalize (statistics from `parts` partial sums around the per-channel shift row `shift`, or
+// the running statistics) then the normalise / pool pass; ab lives at the workspace start
 template <typename E>
-int run(const mcgmil_bn_args* a, hipStream_t s) {
+int finish(const mcgmil_bn_args* a, const float* part, int parts, const E* shift, hipStream_t s) {
     const int C = a->channels;
-    float* ws = static_cast<float*>(a->workspace);
-    float* ab = ws;                      // [2][C]
-    float* part = ws + 2 * C;            // [parts][2][C]
-    const E* x = static_cast<const E*>(a->x);
-    int parts = 0;
-    if (!a->running_mean) {
-        parts = parts_for(a);
-        const long long rpp = (a->rows + parts - 1) / parts;
-        hipLaunchKernelGGL(bn_partial_kernel<E>, dim3(parts), dim3(kThreads), 0, s, x, a->rows, C, rpp, part);
-    }
+    float* ab = static_cast<float*>(a->workspace);   // [2][C]
     hipLaunchKernelGGL(bn_finalize_kernel<E>, dim3((C + kFinCh - 1) / kFinCh), dim3(kThreads), 0, s, part, parts, a->rows,
-                       C, x, a->gamma, a->beta, a->running_mean, a->running_var, a->eps, ab,
+                       C, shift, a->gamma, a->beta, a->running_mean, a->running_var, a->eps, ab,
                        a->batch_mean, a->batch_invstd);
     if (a->pool_kernel > 0) {
         const int Ho = pooled_dim(a->height, a), Wo = pooled_dim(a->width, a);
@@ -342,9 +335,9 @@ int run(const mcgmil_bn_args* a, hipStream_t s) {
         if (want > 8192) want = 8192;
         const long long blocks = (want + unit - 1) / unit * unit;
         auto k = a->relu ? bn_pool_kernel<E, true> : bn_pool_kernel<E, false>;
-        hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kThreads), 0, s, x, static_cast<E*>(a->y),
-                           a->height, a->width, Ho, Wo, a->pool_kernel, a->pool_stride, a->pool_pad,
-                           nvec, C, ab);
+        hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kThreads), 0, s, static_cast<const E*>(a->x),
+                           static_cast<E*>(a->y), a->height, a->width, Ho, Wo, a->pool_kernel,
+                           a->pool_stride, a->pool_pad, nvec, C, ab);
         const hipError_t e = hipGetLastError();
         return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "batchnorm pool launch");
     }
@@ -360,7 +353,39 @@ int run(const mcgmil_bn_args* a, hipStream_t s) {
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "batchnorm launch");
 }
 
+template <typename E>
+int run(const mcgmil_bn_args* a, hipStream_t s) {
+    const int C = a->channels;
+    float* part = static_cast<float*>(a->workspace) + 2 * C;   // [parts][2][C]
+    const E* x = static_cast<const E*>(a->x);
+    int parts = 0;
+    if (!a->running_mean) {
+        parts = parts_for(a);
+        const long long rpp = (a->rows + parts - 1) / parts;
+        hipLaunchKernelGGL(bn_partial_kernel<E>, dim3(parts), dim3(kThreads), 0, s, x, a->rows, C, rpp, part);
+    }
+    return finish<E>(a, part, parts, x, s);   // shift row: x[0, :]
+}
+
 }  // namespace
+
+namespace mcgmil_detail {
+
+// The normalisation half of mcgmil_batchnorm_act for a caller that produced the per-channel
+// partial sums itself (the stem convolution's epilogue): `parts` blocks of [2][C] fp32 sums of
+// (x - shift_c) and (x - shift_c)^2, shift_row the bf16 [C] shift. a->workspace needs 2 * C floats.
+int bn_finish_bf16(const mcgmil_bn_args* a, const float* part, int parts, const void* shift_row,
+                   hipStream_t s) {
+    if (int rc = validate(a)) return rc;
+    if (a->dtype != MCGMIL_BF16) return fail(MCGMIL_E_INVALID, "bn_finish_bf16 needs bf16");
+    if (!a->workspace || a->workspace_bytes < 2 * (size_t)a->channels * sizeof(float))
+        return fail(MCGMIL_E_WORKSPACE, "bn_finish_bf16: workspace smaller than 2 * C floats");
+    if (!a->running_mean && (parts < 1 || !part || !shift_row))
+        return fail(MCGMIL_E_INVALID, "bn_finish_bf16: batch statistics need partials and a shift");
+    return finish<__bf16>(a, part, parts, static_cast<const __bf16*>(shift_row), s);
+}
+
+}  // namespace mcgmil_detail
 
 extern "C" {
 

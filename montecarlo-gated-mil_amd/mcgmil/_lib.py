@@ -29,6 +29,8 @@ EXPORTED = (
     # include/mcgmil_features.h
     "mcgmil_bn_args_size", "mcgmil_bn_workspace_size", "mcgmil_batchnorm_act",
     "mcgmil_conv_args_size", "mcgmil_pack_conv_weights", "mcgmil_conv2d",
+    "mcgmil_stem_args_size", "mcgmil_stem_packed_size", "mcgmil_pack_stem_weights",
+    "mcgmil_stem_workspace_size", "mcgmil_stem_forward",
 )
 
 _vp = ctypes.c_void_p
@@ -80,6 +82,20 @@ class ConvArgs(ctypes.Structure):
         ("kernel_h", ctypes.c_int32), ("kernel_w", ctypes.c_int32), ("stride", ctypes.c_int32),
         ("pad", ctypes.c_int32), ("reserved", ctypes.c_int32),
         ("x", _vp), ("w", _vp), ("y", _vp),
+    ]
+
+
+class StemArgs(ctypes.Structure):
+    """Mirror of struct mcgmil_stem_args (include/mcgmil_features.h)."""
+    _fields_ = [
+        ("batch", ctypes.c_int32), ("in_channels", ctypes.c_int32), ("height", ctypes.c_int32),
+        ("width", ctypes.c_int32), ("out_channels", ctypes.c_int32), ("kernel", ctypes.c_int32),
+        ("stride", ctypes.c_int32), ("pad", ctypes.c_int32), ("pool_kernel", ctypes.c_int32),
+        ("pool_stride", ctypes.c_int32), ("pool_pad", ctypes.c_int32), ("relu", ctypes.c_int32),
+        ("eps", ctypes.c_double), ("x", _vp), ("w", _vp), ("gamma", _vp), ("beta", _vp),
+        ("running_mean", _vp), ("running_var", _vp), ("y", _vp),
+        ("batch_mean", _vp), ("batch_invstd", _vp),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
     ]
 
 
@@ -159,6 +175,19 @@ def load():
     L.mcgmil_pack_conv_weights.restype = ctypes.c_int
     L.mcgmil_conv2d.argtypes = [pc, _vp]
     L.mcgmil_conv2d.restype = ctypes.c_int
+    ps = ctypes.POINTER(StemArgs)
+    L.mcgmil_stem_args_size.restype = ctypes.c_size_t
+    for name in ("mcgmil_stem_packed_size", "mcgmil_stem_workspace_size"):
+        f = getattr(L, name)
+        f.argtypes = [ps, ctypes.POINTER(ctypes.c_size_t)]
+        f.restype = ctypes.c_int
+    L.mcgmil_pack_stem_weights.argtypes = [ps, _vp, ctypes.c_int32, _vp, _vp]
+    L.mcgmil_pack_stem_weights.restype = ctypes.c_int
+    L.mcgmil_stem_forward.argtypes = [ps, _vp]
+    L.mcgmil_stem_forward.restype = ctypes.c_int
+    if L.mcgmil_stem_args_size() != ctypes.sizeof(StemArgs):
+        raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_stem_args)={L.mcgmil_stem_args_size()} "
+                          f"but the ctypes mirror is {ctypes.sizeof(StemArgs)} bytes")
     if L.mcgmil_conv_args_size() != ctypes.sizeof(ConvArgs):
         raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_conv_args)={L.mcgmil_conv_args_size()} "
                           f"but the ctypes mirror is {ctypes.sizeof(ConvArgs)} bytes")

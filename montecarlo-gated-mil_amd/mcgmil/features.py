@@ -18,8 +18,13 @@ MCGMIL_FUSED_BN=0 switches the backbone back to the torch layers (A/B timing and
 padding, 64k input and output channels) on a channels-last bf16 activation as one MFMA
 implicit-GEMM kernel -- the arithmetic of torch.autocast's bf16 convolution (bf16 operands, fp32
 accumulation, one rounding) without MIOpen's per-convolution output fill. `conv_fusable` says when
-it applies; the stem (3 input channels) and everything else keep torch's convolution.
-MCGMIL_NATIVE_CONV=0 switches it off.
+it applies. MCGMIL_NATIVE_CONV=0 switches it off.
+
+`stem` runs the torchvision stem maxpool(relu(bn1(conv1(x)))) (7x7/2 convolution of the 3-channel
+instances) as one library call (mcgmil_stem_forward): an MFMA implicit GEMM straight from the NCHW
+bf16 instances the patcher writes, with the BatchNorm statistics accumulated in its epilogue, then
+the fused normalise + ReLU + max-pool pass. `stem_fusable` says when it applies (else the torch
+layers run); MCGMIL_NATIVE_STEM=0 switches it off.
 """
 import ctypes
 import os
@@ -225,3 +230,121 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool,
         y = y + residual
     y = torch.relu(y) if relu else y
     return y if pool is None else pool(y)
+
+
+def stem_enabled() -> bool:
+    return os.environ.get("MCGMIL_NATIVE_STEM", "1") != "0"
+
+
+def stem_fusable(conv: nn.Module, bn: nn.Module, pool: Optional[nn.Module], x: torch.Tensor) -> bool:
+    """A CUDA [N, C<=4, H, W] activation that torch would convolve in bf16, a bias-free
+    Conv2d(C, 64, k, stride 2) with k + (pad & 1) <= 8 and OW <= 125, a BatchNorm2d(64) the fused
+    BN handles (see fusable), and a plain max-pool (or none); no autograd."""
+    if not (stem_enabled() and isinstance(conv, nn.Conv2d) and isinstance(bn, nn.BatchNorm2d)):
+        return False
+    if not (x.is_cuda and x.dim() == 4 and x.dtype in _DT and x.numel() > 0):
+        return False
+    if conv.groups != 1 or conv.bias is not None or conv.padding_mode != "zeros":
+        return False
+    if _square(conv.dilation) != 1 or _square(conv.stride) != 2 or not isinstance(conv.padding, tuple) \
+            or _square(conv.padding) is None or _square(conv.kernel_size) is None:
+        return False
+    k, pad = conv.kernel_size[0], conv.padding[0]
+    N, C, H, W = x.shape
+    if C != conv.in_channels or not 1 <= C <= 4 or conv.out_channels != 64 or bn.num_features != 64:
+        return False
+    if k + (pad & 1) > 8 or W % 2 or H + 2 * pad < k or W + 2 * pad < k or (W + 2 * pad - k) // 2 + 1 > 125:
+        return False
+    if pool is not None and _pool_params(pool) is None:
+        return False
+    bf16 = x.dtype == torch.bfloat16 or conv.weight.dtype == torch.bfloat16 or \
+        (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+    if not bf16:
+        return False
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in conv.parameters())
+                                    or any(p.requires_grad for p in bn.parameters())):
+        return False
+    if bn.training and bn.track_running_stats and bn.running_mean is not None:
+        return False
+    return True
+
+
+def _stem_args(conv: nn.Conv2d, x: torch.Tensor) -> "_lib.StemArgs":
+    a = _lib.StemArgs()
+    a.batch, a.in_channels, a.height, a.width = x.shape
+    a.out_channels, a.kernel = conv.out_channels, conv.kernel_size[0]
+    a.stride, a.pad = conv.stride[0], conv.padding[0]
+    return a
+
+
+def packed_stem_weight(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """The stem weight in the kernel's MFMA fragment order (bf16), cached on the module and keyed
+    by the weight's version."""
+    w = conv.weight.detach()
+    key = (w.data_ptr(), w._version, w.dtype, x.device)
+    cached = getattr(conv, "_mcgmil_stem_packed", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    L = _lib.load()
+    a = _stem_args(conv, x)
+    n = ctypes.c_size_t()
+    _lib.check(L.mcgmil_stem_packed_size(ctypes.byref(a), ctypes.byref(n)), "mcgmil_stem_packed_size")
+    wc = w.to(device=x.device).contiguous()
+    if wc.dtype not in _DT:
+        wc = wc.float()
+    packed = torch.empty(n.value, dtype=torch.uint8, device=x.device)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    _lib.check(L.mcgmil_pack_stem_weights(ctypes.byref(a), ctypes.c_void_p(wc.data_ptr()), _DT[wc.dtype],
+                                          ctypes.c_void_p(packed.data_ptr()), stream),
+               "mcgmil_pack_stem_weights")
+    conv._mcgmil_stem_packed = (key, packed)
+    return packed
+
+
+def stem(conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool, pool: Optional[nn.MaxPool2d],
+         x: torch.Tensor) -> torch.Tensor:
+    """pool?(relu?(bn(conv(x)))) of NCHW instances (see stem_fusable) -> channels-last bf16."""
+    if not stem_fusable(conv, bn, pool, x):
+        raise ValueError("stem needs a CUDA [N, C<=4, H, W] bf16 (or autocast) input, a bias-free "
+                         "stride-2 Conv2d(C, 64) with k + (pad & 1) <= 8 and OW <= 125, a "
+                         "BatchNorm2d(64) and a square max-pool, without autograd (see stem_fusable)")
+    L = _lib.load()
+    dev = x.device
+    xb = x.to(torch.bfloat16).contiguous()
+    a = _stem_args(conv, xb)
+    N, _, H, W = xb.shape
+    OH = (H + 2 * a.pad - a.kernel) // 2 + 1
+    OW = (W + 2 * a.pad - a.kernel) // 2 + 1
+    PH, PW = OH, OW
+    if pool is not None:
+        k, st, pd = _pool_params(pool)
+        a.pool_kernel, a.pool_stride, a.pool_pad = k, st, pd
+        PH, PW = (OH + 2 * pd - k) // st + 1, (OW + 2 * pd - k) // st + 1
+    use_batch = bn.training or bn.running_mean is None or bn.running_var is None
+    gamma = _f32(bn.weight, dev) if bn.affine else None
+    beta = _f32(bn.bias, dev) if bn.affine else None
+    rmean = None if use_batch else _f32(bn.running_mean, dev)
+    rvar = None if use_batch else _f32(bn.running_var, dev)
+    w = packed_stem_weight(conv, xb)
+    y = torch.empty((N, 64, PH, PW), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
+    p = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    a.x, a.w, a.y = p(xb), p(w), p(y)
+    a.gamma, a.beta, a.running_mean, a.running_var = p(gamma), p(beta), p(rmean), p(rvar)
+    a.eps, a.relu = float(bn.eps), int(bool(relu))
+    n = ctypes.c_size_t()
+    _lib.check(L.mcgmil_stem_workspace_size(ctypes.byref(a), ctypes.byref(n)), "mcgmil_stem_workspace_size")
+    ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
+    a.workspace, a.workspace_bytes = p(ws), n.value
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    _lib.check(L.mcgmil_stem_forward(ctypes.byref(a), stream), "mcgmil_stem_forward")
+    return y
+
+
+def run_stem(conv: nn.Module, bn: nn.Module, pool: Optional[nn.Module], x: torch.Tensor) -> torch.Tensor:
+    """The backbone's stem: the fused kernel when `stem_fusable`, else conv + bn_act (on the GPU
+    with a channels-last activation, so the blocks after it stay on the fused path)."""
+    if stem_fusable(conv, bn, pool, x):
+        return stem(conv, bn, True, pool, x)
+    if x.is_cuda and x.dim() == 4:
+        x = x.contiguous(memory_format=torch.channels_last)
+    return bn_act(bn, conv(x), True, pool=pool)

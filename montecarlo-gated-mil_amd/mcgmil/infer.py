@@ -96,7 +96,7 @@ def mc_predict_image(model, patcher, image: torch.Tensor, T: int = 100, seed: Op
     ctx = torch.autocast("cuda", dtype=features_dtype) if features_dtype is not None \
         else contextlib.nullcontext()
     with ctx:
-        H = model.extract_features(inst.contiguous(memory_format=torch.channels_last)[None])
+        H = model.extract_features(inst[None])      # NCHW: the stem kernel reads it as written
     _stage(events, "features", stream)
     Y, A, st = model.mc_inference_features(H[0].float(), T=T, seed=seed, return_stats=True)
     _stage(events, "mcdo_head", stream)

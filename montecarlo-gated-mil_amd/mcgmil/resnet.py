@@ -10,7 +10,9 @@ Identity (model.py:179) and, in infer.py, forces every BatchNorm to batch statis
 ImageNet weights cannot be downloaded offline: `pretrained=True` builds the same architecture
 with random initialisation and warns (load a checkpoint to get trained weights).
 
-Every `relu?(bn(conv(x)) [+ identity])` of the blocks goes through `features.run_conv` and
+The stem `maxpool(relu(bn1(conv1(x))))` goes through `features.run_stem` (one fused MFMA
+convolution + statistics + BN/ReLU/pool call on the GPU) and every
+`relu?(bn(conv(x)) [+ identity])` of the blocks goes through `features.run_conv` and
 `features.bn_act`: on the GPU with channels-last bf16 activations they are the MFMA
 implicit-GEMM convolution and one fused HIP BatchNorm(+add)(+ReLU) (include/mcgmil_features.h);
 elsewhere (CPU, autograd, fp32) they are the torch layers.
@@ -20,7 +22,7 @@ import warnings
 import torch
 import torch.nn as nn
 
-from .features import bn_act, run_conv
+from .features import bn_act, run_conv, run_stem
 
 
 class Identity(nn.Module):
@@ -119,7 +121,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = bn_act(self.bn1, self.conv1(x), True, pool=self.maxpool)
+        x = run_stem(self.conv1, self.bn1, self.maxpool, x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

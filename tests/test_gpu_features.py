@@ -141,6 +141,7 @@ def _backbone_features(cuda, fused, dtype):
     from mcgmil.resnet import build_backbone, deactivate_batchnorm, Identity
     os.environ["MCGMIL_FUSED_BN"] = "1" if fused else "0"
     os.environ["MCGMIL_NATIVE_CONV"] = "1" if fused else "0"
+    os.environ["MCGMIL_NATIVE_STEM"] = "1" if fused else "0"
     try:
         torch.manual_seed(0)
         net = build_backbone("r18", pretrained=False)
@@ -158,6 +159,7 @@ def _backbone_features(cuda, fused, dtype):
     finally:
         os.environ.pop("MCGMIL_FUSED_BN", None)
         os.environ.pop("MCGMIL_NATIVE_CONV", None)
+        os.environ.pop("MCGMIL_NATIVE_STEM", None)
 
 
 def test_backbone_fused_bn_matches_torch_layers(cuda):
