@@ -100,7 +100,7 @@ int geometry(const mcgmil_stem_args* a, Geometry* out) {
     g.pitch = (g.wd + 63) / 64 * 64 + 16;   // whole 64-dword DMA pieces, 16 (mod 64)
     g.plane = g.RR * g.pitch;
     while ((g.plane - g.k * g.pitch) % 64 != 0) ++g.plane;
-    G.lds = (size_t)2 * g.Cin * g.plane * 4;
+    G.lds = (size_t)2 * g.Cin * g.plane * 4 + (size_t)kTH * 16 * kCout * 2;   // + epilogue scratch
     if (G.lds > (size_t)kLdsBytes) return fail(MCGMIL_E_UNSUPPORTED, "stem tile exceeds 64 KiB of LDS");
     g.TPI = (OH + kTH - 1) / kTH;
     const long long tiles = (long long)g.N * g.TPI;
@@ -143,31 +143,33 @@ __global__ void pack_stem_weights_kernel(const T* __restrict__ w, int Cin, int k
     }
 }
 
-// Zeroes the staging's padding source and, with batch statistics, writes the BatchNorm shift row: the convolution at pixel (0, OH/2, OW/2), fp32, rounded to bf16 (any
-// value near the channel mean keeps the shifted sums well conditioned; all partials share it).
-__global__ void stem_prep_kernel(const StemGeom g, int KS, int stats) {
-    const int c = threadIdx.x;
-    if (c >= kCout) return;
-    const_cast<uint32_t*>(g.zero)[c] = 0u;
+// Zeroes the staging's padding source and, with batch statistics, writes the BatchNorm shift
+// row: the convolution at pixel (0, OH/2, OW/2), fp32, rounded to bf16 (any value near the
+// channel mean keeps the shifted sums well conditioned; all partials share it).
+__global__ __launch_bounds__(256) void stem_prep_kernel(const StemGeom g, int KS, int stats) {
+    __shared__ float red[4][kCout];
+    const int tid = threadIdx.x, c = tid & 63, part = tid >> 6;
+    if (tid < kCout) const_cast<uint32_t*>(g.zero)[tid] = 0u;
     if (!stats) return;
     const int oh = g.OH / 2, ow = g.OW / 2, e = g.P - g.pad;
     const __bf16* wp = reinterpret_cast<const __bf16*>(g.w);
     float acc = 0.f;
-    for (int s = 0; s < KS; ++s)
-        for (int q = 0; q < 4; ++q) {
-            const int r = 4 * s + q;
-            if (r >= g.Cin * g.k) continue;
-            const int ci = r / g.k, kh = r - ci * g.k, ih = 2 * oh - g.pad + kh;
-            if (ih < 0 || ih >= g.H) continue;
-            for (int j = 0; j < 8; ++j) {
-                const int iw = 2 * ow - g.pad + (j - e);
-                if (j - e < 0 || j - e >= g.k || iw < 0 || iw >= g.W) continue;
-                const float xv = (float)g.x[((size_t)ci * g.H + ih) * g.W + iw];
-                const float wv = (float)wp[((size_t)(s * 4 + c / 16) * 64 + (c & 15) + 16 * q) * 8 + j];
-                acc = fmaf(xv, wv, acc);
-            }
+    for (int r = part; r < g.Cin * g.k; r += 4) {       // (ci, kh) rows split over 4 waves
+        const int s = r >> 2, q = r & 3, ci = r / g.k, kh = r - ci * g.k, ih = 2 * oh - g.pad + kh;
+        if (ih < 0 || ih >= g.H) continue;
+        for (int j = 0; j < 8; ++j) {
+            const int iw = 2 * ow - g.pad + (j - e);
+            if (j - e < 0 || j - e >= g.k || iw < 0 || iw >= g.W) continue;
+            const float xv = (float)g.x[((size_t)ci * g.H + ih) * g.W + iw];
+            const float wv = (float)wp[((size_t)(s * 4 + c / 16) * 64 + (c & 15) + 16 * q) * 8 + j];
+            acc = fmaf(xv, wv, acc);
         }
-    const_cast<__bf16*>(g.shift)[c] = (__bf16)acc;
+    }
+    red[part][c] = acc;
+    __syncthreads();
+    if (tid < kCout)
+        const_cast<__bf16*>(g.shift)[c] = (__bf16)(red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+    (void)KS;
 }
 
 template <int KS, bool STATS>
@@ -211,8 +213,12 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
     auto stage = [&](int t, int buf) {
         const int n = t / g.TPI, oh0 = (t - n * g.TPI) * kTH;
         uint32_t* L = lds + buf * buf_dw;
-        for (int sr = wave; sr < nsr; sr += kTH) {
-            const int ci = sr / g.RR, rr = sr - ci * g.RR;
+        int ci = 0, rr = wave;                 // row sr = ci * RR + rr, stepped by kTH (RR >= kTH)
+        for (int sr = wave; sr < nsr; sr += kTH, rr += kTH) {
+            if (rr >= g.RR) {
+                rr -= g.RR;
+                ++ci;
+            }
             const int ih = 2 * oh0 - g.pad + rr;
             const bool rok = ih >= 0 && ih < g.H;
             const uint32_t* row = reinterpret_cast<const uint32_t*>(g.x) +
@@ -229,12 +235,15 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
     };
 
     const int FR = (g.OW + 15) >> 4;
+    __bf16* scratch = reinterpret_cast<__bf16*>(lds + 2 * buf_dw) + wave * 16 * kCout;   // 2 KiB per wave
     if (t0 < t1) stage(t0, 0);
     __syncthreads();
     for (int t = t0; t < t1; ++t) {
         const int cur = (t - t0) & 1;
         const bool more = t + 1 < t1;
+#ifndef MCGMIL_STEM_LATE_STAGE   // A/B variant: stage the next tile after this one's compute
         if (more) stage(t + 1, cur ^ 1);
+#endif
         const int n = t / g.TPI, oh = (t - n * g.TPI) * kTH + wave;
         if (oh < g.OH) {
             const uint32_t* L = lds + cur * buf_dw;
@@ -254,27 +263,46 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
                     for (int i = 0; i < 4; ++i)
                         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s][i], b, acc[i], 0, 0, 0);
                 }
-                if (ow < g.OW) {
-                    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-                    __bf16* dst = yrow + (size_t)ow * kCout + 4 * q;
+                // epilogue: round, transpose the 16 pixels x 64 channels through the wave's LDS
+                // scratch (pixel rows of 128 B, 16-B chunks XOR-swizzled by pixel) and store
+                // each pixel row as 16-B pieces, 1 KiB contiguous per wave-instruction
+                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                const bool valid = ow < g.OW;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        bf16x4 o;
+                for (int i = 0; i < 4; ++i) {
+                    bf16x4 o;
 #pragma unroll
-                        for (int v = 0; v < 4; ++v) o[v] = (__bf16)acc[i][v];
-                        *reinterpret_cast<bf16x4*>(dst + 16 * i) = o;
-                        if (STATS) {
+                    for (int v = 0; v < 4; ++v) o[v] = (__bf16)acc[i][v];
+                    const int c = 2 * i + (q >> 1);
+                    *reinterpret_cast<bf16x4*>(scratch + p * 64 + ((c ^ (p & 7)) << 3) + ((q & 1) << 2)) = o;
+                    if (STATS && valid) {
 #pragma unroll
-                            for (int v = 0; v < 4; ++v) {
-                                const float d = (float)o[v] - sh[4 * i + v];
-                                S[4 * i + v] += d;
-                                SS[4 * i + v] = fmaf(d, d, SS[4 * i + v]);
-                            }
+                        for (int v = 0; v < 4; ++v) {
+                            const float d = (float)o[v] - sh[4 * i + v];
+                            S[4 * i + v] += d;
+                            SS[4 * i + v] = fmaf(d, d, SS[4 * i + v]);
                         }
                     }
                 }
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int pp = (lane >> 3) + 8 * h, c = lane & 7;
+                    const bf16x8 v = *reinterpret_cast<const bf16x8*>(scratch + pp * 64 + ((c ^ (pp & 7)) << 3));
+#ifndef MCGMIL_STEM_NOSTORE   // timing-only variant: no activation stores
+                    if (16 * f + pp < g.OW)
+                        *reinterpret_cast<bf16x8*>(yrow + (size_t)(16 * f + pp) * kCout + 8 * c) = v;
+#else
+                    if (v[0] == (__bf16)12345.f) yrow[0] = v[1];
+#endif
+                }
+                asm volatile("" ::: "memory");
             }
         }
+#ifdef MCGMIL_STEM_LATE_STAGE
+        if (more) stage(t + 1, cur ^ 1);
+#endif
         __syncthreads();
     }
 
@@ -417,7 +445,7 @@ int mcgmil_stem_forward(const mcgmil_stem_args* a, void* stream) {
     g.zero = reinterpret_cast<const uint32_t*>(ws + c.shift + 128);
     g.part = reinterpret_cast<float*>(ws + c.part);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(stem_prep_kernel, dim3(1), dim3(kCout), 0, s, g, G.KS, (int)stats);
+    hipLaunchKernelGGL(stem_prep_kernel, dim3(1), dim3(256), 0, s, g, G.KS, (int)stats);
     switch (G.KS) {
         case 1: launch_conv<1>(g, c.grid, G.lds, stats, s); break;
         case 2: launch_conv<2>(g, c.grid, G.lds, stats, s); break;

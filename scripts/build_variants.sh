@@ -18,7 +18,7 @@ for spec in "$@"; do
     fi
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -I"$inc" \
         -Xclang -target-feature -Xclang -packed-fp32-ops $defs \
-        -o "$OUT/$name.so" "$src/mcgmil.hip" "$src/mcgmil_image.hip" $( [ -f "$src/mcgmil_bn.hip" ] && echo "$src/mcgmil_bn.hip" ) 2>&1 | grep -v packed-fp32-ops || true &
+        -o "$OUT/$name.so" "$src/mcgmil.hip" "$src/mcgmil_image.hip" $(for f in mcgmil_bn.hip mcgmil_conv.hip mcgmil_stem.hip; do [ -f "$src/$f" ] && echo "$src/$f"; done) 2>&1 | grep -v packed-fp32-ops || true &
 done
 wait
 ls "$OUT"
