@@ -18,6 +18,11 @@
 // under torch.autocast, up to the summation order.
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <mutex>
 #include <string>
 
 #include "../../include/mcgmil_features.h"
@@ -31,7 +36,7 @@ using mcgmil_detail::fail;
 using mcgmil_detail::hip_fail;
 
 constexpr int kConvThreads = 256;
-constexpr int kBM = 128;            // output pixels per tile
+constexpr int kBM = 256;            // largest pixel tile (host-side size check)
 constexpr int kBK = 64;             // K elements per stage (one 128-byte row per pixel/channel)
 constexpr int kRowBytes = kBK * 2;
 
@@ -63,28 +68,32 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-template <int BN>
+// BM pixels x BN channels per workgroup; the 4 waves form a WGM x (4 / WGM) grid, each owning
+// BM / WGM pixels x BN / (4 / WGM) channels (64 x 64 for the 128 x 128 and 256 x 64 shapes).
+template <int BM, int BN, int WGM>
 __global__ __launch_bounds__(kConvThreads, 2) void conv_kernel(const ConvGeom g) {
-    constexpr int STAGE = (kBM + BN) * kRowBytes;     // A rows then B rows
+    constexpr int WGN = 4 / WGM;
+    constexpr int STAGE = (BM + BN) * kRowBytes;      // A rows then B rows
+    constexpr int NA = BM / 32;                       // A chunks per thread per stage
     constexpr int NB = BN / 32;                       // B chunks per thread per stage
-    constexpr int WN = BN / 2;                        // channels per wave
+    constexpr int WM = BM / WGM, WN = BN / WGN;       // wave tile
     constexpr int FI = WN / 16;                       // channel fragments per wave
-    constexpr int FJ = 4;                             // pixel fragments per wave (64 pixels)
-    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
+    constexpr int FJ = WM / 16;                       // pixel fragments per wave
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t = xcd_remap((int)blockIdx.x, (int)gridDim.x);
     if (t >= g.tiles) return;
     const int tm = t / g.tiles_n, tn = t - tm * g.tiles_n;
-    const int m0 = tm * kBM, n0 = tn * BN;
+    const int m0 = tm * BM, n0 = tn * BN;
 
     // ---- staging assignment: chunk c of rows (tid >> 3) + 32 i
     const int c = tid & 7, r0 = tid >> 3;
     const __amdgpu_buffer_rsrc_t xr = make_rsrc(g.x, g.x_bytes);
     const __amdgpu_buffer_rsrc_t wr = make_rsrc(g.w, g.w_bytes);
-    int pix_base[4], ih0[4], iw0[4];
+    int pix_base[NA], ih0[NA], iw0[NA];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NA; ++i) {
         const int m = m0 + r0 + 32 * i;
         const int mm = m < g.M ? m : 0;
         const int n = mm / (g.OH * g.OW);
@@ -100,12 +109,12 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_kernel(const ConvGeom g)
 #pragma unroll
     for (int i = 0; i < NB; ++i) wrow[i] = ((uint32_t)(n0 + r0 + 32 * i) * K + (uint32_t)c * 8u) * 2u;
 
-    uint4 ra[4], rb[NB];
+    uint4 ra[NA], rb[NB];
     auto load = [&](int kt) {
         const int khw = kt / g.cin_tiles, cc = kt - khw * g.cin_tiles;
         const int kh = khw / g.KW, kw = khw - kh * g.KW;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NA; ++i) {
             const int ih = ih0[i] + kh, iw = iw0[i] + kw;
             const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
             const uint32_t off = ((uint32_t)(pix_base[i] + ih * g.W + iw) * (uint32_t)g.Cin +
@@ -120,15 +129,15 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_kernel(const ConvGeom g)
     };
     auto store = [&](int buf) {
         unsigned char* A = smem + buf * STAGE;
-        unsigned char* B = A + kBM * kRowBytes;
+        unsigned char* B = A + BM * kRowBytes;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(A + swz(r0 + 32 * i, c)) = ra[i];
+        for (int i = 0; i < NA; ++i) *reinterpret_cast<uint4*>(A + swz(r0 + 32 * i, c)) = ra[i];
 #pragma unroll
         for (int i = 0; i < NB; ++i) *reinterpret_cast<uint4*>(B + swz(r0 + 32 * i, c)) = rb[i];
     };
 
-    // ---- compute assignment: wave (wm, wn) owns pixels wm*64.. and channels wn*WN..
-    const int wm = wave >> 1, wn = wave & 1;
+    // ---- compute assignment: wave (wm, wn) owns pixels wm*WM.. and channels wn*WN..
+    const int wm = wave / WGN, wn = wave % WGN;
     f32x4 acc[FI][FJ];
 #pragma unroll
     for (int i = 0; i < FI; ++i)
@@ -137,7 +146,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_kernel(const ConvGeom g)
 
     auto compute = [&](int buf) {
         const unsigned char* A = smem + buf * STAGE;
-        const unsigned char* B = A + kBM * kRowBytes;
+        const unsigned char* B = A + BM * kRowBytes;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int kq = ks * 4 + (lane >> 4);
@@ -147,7 +156,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_kernel(const ConvGeom g)
                 wf[i] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WN + i * 16 + (lane & 15), kq));
 #pragma unroll
             for (int j = 0; j < FJ; ++j)
-                xf[j] = *reinterpret_cast<const bf16x8*>(A + swz(wm * 64 + j * 16 + (lane & 15), kq));
+                xf[j] = *reinterpret_cast<const bf16x8*>(A + swz(wm * WM + j * 16 + (lane & 15), kq));
 #pragma unroll
             for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -170,7 +179,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_kernel(const ConvGeom g)
     // ---- epilogue: lane holds channels 4*(lane>>4)+v of pixel (lane & 15) per fragment
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
-        const int m = m0 + wm * 64 + j * 16 + (lane & 15);
+        const int m = m0 + wm * WM + j * 16 + (lane & 15);
         if (m >= g.M) continue;
         __bf16* dst = g.y + (size_t)m * g.Cout + n0 + wn * WN + 4 * (lane >> 4);
 #pragma unroll
@@ -182,6 +191,406 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_kernel(const ConvGeom g)
             *reinterpret_cast<bf16x4*>(dst + i * 16) = o;
         }
     }
+}
+
+// ---- LDS-DMA variant: 8 waves, BM x BN tiles, three LDS stages filled by buffer_load ... lds
+// (no staging registers, no ds_write pass). Each wave-instruction moves 1 KiB = 8 rows of 128 B
+// straight into LDS (lane L: row L / 8, slot L % 8); the XOR swizzle goes on the SOURCE chunk
+// (slot s of row r holds chunk s ^ ((r >> 1) & 7)), so the fragment reads are the same swz() as
+// above. Out-of-image taps use an out-of-range offset: the descriptor's range check returns 0.
+// One persistent workgroup per CU walks its tiles' (tile, K tile) steps as one stream: step s + 2 is
+// issued right after the barrier that opens step s (so each DMA has two compute phases to land, and
+// the next tile's first stages load under this tile's last steps and epilogue); the wait is a
+// counted vmcnt (the other stage stays in flight) before a raw s_barrier (a __syncthreads would
+// drain both).
+constexpr int kDmaThreads = 512;
+
+int cu_count() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+    if (dev < 64) {
+        const int c = cache[dev].load(std::memory_order_relaxed);
+        if (c > 0) return c;
+    }
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    if (dev < 64) cache[dev].store(cus, std::memory_order_relaxed);
+    return cus;
+}
+
+// 16 bytes per lane from a buffer straight into LDS at the wave-uniform base + 16 * lane. The
+// builtin only exists in the device pass; the host pass must still see a kernel body to emit the
+// launch stub, hence the guard (device-only code, not a second platform path).
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t voff, uint32_t soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+#else
+    (void)r; (void)lds; (void)voff; (void)soff;
+#endif
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WGM, int NS>
+__global__ __launch_bounds__(kDmaThreads, 1) void conv_dma_kernel(const ConvGeom g) {
+    constexpr int WGN = 8 / WGM;
+    constexpr int STAGE = (BM + BN) * kRowBytes;
+    constexpr int PA = BM / 64, PB = BN / 64;         // 1-KiB pieces per wave per stage (A, B)
+    constexpr int WM = BM / WGM, WN = BN / WGN;
+    constexpr int FI = WN / 16, FJ = WM / 16;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // persistent: workgroup b owns the contiguous tiles [t0, t1) (consecutive tiles are the column
+    // tiles of one pixel tile: same input rows, same L2); the (tile, K tile) steps form one stream
+    const int t0 = (int)((long long)blockIdx.x * g.tiles / gridDim.x);
+    const int t1 = (int)((long long)(blockIdx.x + 1) * g.tiles / gridDim.x);
+    const int steps = (t1 - t0) * g.KT;
+    if (steps <= 0) return;
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(g.x, g.x_bytes);
+    const __amdgpu_buffer_rsrc_t wr = make_rsrc(g.w, g.w_bytes);
+    const uint32_t K = (uint32_t)(g.KH * g.KW * g.Cin);
+
+    // issue side: the DMA addresses of the tile being fetched (runs two steps ahead of compute)
+    int itile = -1;
+    int pix_base[PA], ih0[PA], iw0[PA], cha[PA];
+    uint32_t wrow[PB];
+    auto setup = [&](int tile) {
+        itile = tile;
+        const int tm = tile / g.tiles_n, tn = tile - tm * g.tiles_n;
+#pragma unroll
+        for (int j = 0; j < PA; ++j) {
+            const int r = 8 * (wave + 8 * j) + (lane >> 3);
+            const int m = tm * BM + r;
+            const int mm = m < g.M ? m : 0;
+            const int n = mm / (g.OH * g.OW);
+            const int rem = mm - n * g.OH * g.OW;
+            const int oh = rem / g.OW, ow = rem - oh * g.OW;
+            pix_base[j] = n * g.H * g.W;
+            ih0[j] = m < g.M ? oh * g.stride - g.pad : -(1 << 28);   // rows past M load zeros
+            iw0[j] = ow * g.stride - g.pad;
+            cha[j] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;     // source chunk of this lane's LDS slot
+        }
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            const int r = 8 * (wave + 8 * j) + (lane >> 3);
+            wrow[j] = ((uint32_t)(tn * BN + r) * K + (uint32_t)(((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
+        }
+    };
+    auto issue = [&](int step, int buf) {
+        const int tile = t0 + step / g.KT, kt = step - (tile - t0) * g.KT;
+        if (tile != itile) setup(tile);
+        const int khw = kt / g.cin_tiles, cc = kt - khw * g.cin_tiles;
+        const int kh = khw / g.KW, kw = khw - kh * g.KW;
+        unsigned char* A = smem + buf * STAGE;
+        unsigned char* B = A + BM * kRowBytes;
+#pragma unroll
+        for (int j = 0; j < PA; ++j) {
+            const int ih = ih0[j] + kh, iw = iw0[j] + kw;
+            const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+            const uint32_t off = ((uint32_t)(pix_base[j] + ih * g.W + iw) * (uint32_t)g.Cin +
+                                  (uint32_t)(cc * 64 + cha[j])) * 2u;
+            dma16(xr, A + (wave + 8 * j) * 1024, ok ? off : 0x80000000u, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < PB; ++j)
+            dma16(wr, B + (wave + 8 * j) * 1024, wrow[j], (uint32_t)kt * (kBK * 2u));
+    };
+
+    const int wm = wave / WGN, wn = wave % WGN;
+    f32x4 acc[FI][FJ];
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto compute = [&](int buf) {
+        const unsigned char* A = smem + buf * STAGE;
+        const unsigned char* B = A + BM * kRowBytes;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int kq = ks * 4 + (lane >> 4);
+            bf16x8 wf[FI], xf[FJ];
+#pragma unroll
+            for (int i = 0; i < FI; ++i)
+                wf[i] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WN + i * 16 + (lane & 15), kq));
+#pragma unroll
+            for (int j = 0; j < FJ; ++j)
+                xf[j] = *reinterpret_cast<const bf16x8*>(A + swz(wm * WM + j * 16 + (lane & 15), kq));
+#pragma unroll
+            for (int i = 0; i < FI; ++i)
+#pragma unroll
+                for (int j = 0; j < FJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+        }
+    };
+    // lane holds channels 4*(lane>>4)+v of pixel (lane & 15) per fragment
+    auto epilogue = [&](int tile) {
+        const int tm = tile / g.tiles_n, tn = tile - tm * g.tiles_n;
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+            const int m = tm * BM + wm * WM + j * 16 + (lane & 15);
+            if (m >= g.M) continue;
+            __bf16* dst = g.y + (size_t)m * g.Cout + tn * BN + wn * WN + 4 * (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < FI; ++i) {
+                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                bf16x4 o;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) o[v] = (__bf16)acc[i][j][v];
+                *reinterpret_cast<bf16x4*>(dst + i * 16) = o;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+            for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+
+    // NS LDS stages: step st + NS - 1 is issued into the stage step st - 1 used
+    issue(0, 0);
+    if (NS == 3 && steps > 1) issue(1, 1);
+    int buf = 0, kt = 0, tile = t0;
+    for (int st = 0; st < steps; ++st) {
+        // step st landed (counted: the next step's DMAs may stay in flight; vmcnt retires in order)
+        if (NS == 3 && st + 1 < steps) wait_vmcnt<PA + PB>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (st + NS - 1 < steps) issue(st + NS - 1, buf == 0 ? NS - 1 : buf - 1);
+        compute(buf);
+        buf = buf == NS - 1 ? 0 : buf + 1;
+        if (++kt == g.KT) {
+            epilogue(tile);
+            kt = 0;
+            ++tile;
+        }
+    }
+}
+
+template <int BM, int BN, int WGM, int NS>
+int launch_conv_dma(const ConvGeom& g0, hipStream_t s) {
+    static std::once_flag once;
+    auto k = conv_dma_kernel<BM, BN, WGM, NS>;
+    std::call_once(once, [&] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    ConvGeom g = g0;
+    g.tiles_n = g.Cout / BN;
+    const long long tiles = (long long)((g.M + BM - 1) / BM) * g.tiles_n;
+    if (tiles >= (1ll << 31)) return fail(MCGMIL_E_UNSUPPORTED, "too many tiles");
+    g.tiles = (int)tiles;
+    const size_t lds = (size_t)NS * (BM + BN) * kRowBytes;
+    const int grid = (int)(tiles < cu_count() ? tiles : cu_count());    // one workgroup per CU
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kDmaThreads), lds, s, g);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "conv_dma_kernel launch");
+}
+
+template <int BM, int BN, int WGM>
+int launch_conv(const ConvGeom& g0, hipStream_t s) {
+    static std::once_flag once;
+    auto k = conv_kernel<BM, BN, WGM>;
+    std::call_once(once, [&] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    ConvGeom g = g0;
+    g.tiles_n = g.Cout / BN;
+    const long long tiles = (long long)((g.M + BM - 1) / BM) * g.tiles_n;
+    if (tiles >= (1ll << 31)) return fail(MCGMIL_E_UNSUPPORTED, "too many tiles");
+    g.tiles = (int)tiles;
+    const size_t lds = (size_t)2 * (BM + BN) * kRowBytes;
+    hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(kConvThreads), lds, s, g);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "conv_kernel launch");
+}
+
+// ---- 3x3 / stride 1 / pad 1, 64 -> 64 channels (ResNet layer 1): halo-tile kernel.
+// The generic kernels fetch every input pixel once per tap (9x), which makes these layers L2-
+// bandwidth-bound (~520 TFLOP/s). Here a persistent workgroup (8 waves, one per CU) keeps the
+// whole 64 x 576 weight matrix in registers (each wave its 32 channels: 36 fragments) and, per
+// 256-pixel tile, DMAs the tile's input rows ONCE into LDS as a zero-padded patch: padded rows
+// P = n (H + 2) + ih + 1 of W + 2 pixels x 128 B (XOR-swizzled by patch pixel). All 9 taps then
+// read their A fragments from the patch at a tap offset -- no barrier inside a tile, 5x less L2
+// traffic per FLOP. The next tile's patch loads into the other buffer during this tile.
+constexpr int kHaloBM = 256;
+
+__device__ __forceinline__ uint32_t swz_lin(int p, int c) {     // swz() for a patch pixel index
+    return (uint32_t)p * kRowBytes + (uint32_t)((c ^ ((p >> 1) & 7)) << 4);
+}
+
+struct HaloGeom {
+    ConvGeom g;
+    int WP;         // W + 2 (padded row width)
+    int NR;         // padded rows per patch (max over tiles)
+    int patch_px;   // NR * WP
+};
+
+__global__ __launch_bounds__(kDmaThreads, 1) void conv3x3c64_kernel(const HaloGeom hg) {
+    const ConvGeom& g = hg.g;
+    constexpr int FI = 2, FJ = 4, KSTEPS = 18;          // wave: 64 pixels x 32 channels
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int t0 = (int)((long long)blockIdx.x * g.tiles / gridDim.x);
+    const int t1 = (int)((long long)(blockIdx.x + 1) * g.tiles / gridDim.x);
+    if (t0 >= t1) return;
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(g.x, g.x_bytes);
+    const int HP = g.H + 2, WP = hg.WP;
+    const size_t patch_bytes = (size_t)hg.patch_px * kRowBytes;
+
+    // weights -> registers: K step s = (tap, half) covers k = 32 s .. 32 s + 31
+    bf16x8 wf[KSTEPS][FI];
+#pragma unroll
+    for (int st = 0; st < KSTEPS; ++st)
+#pragma unroll
+        for (int i = 0; i < FI; ++i) {
+            const int co = wn * 32 + i * 16 + (lane & 15);
+            wf[st][i] = *reinterpret_cast<const bf16x8*>(g.w + (size_t)co * 576 + st * 32 + (lane >> 4) * 8);
+        }
+
+    // No per-tile integer division on the vector side: a tile's first pixel (n0, oh0, ow0) is
+    // scalar math, every lane-dependent offset below is split into (rows, cols) once per kernel and
+    // carried forward per tile / per DMA piece.
+    const int OHW = g.OH * g.OW;
+    int dq[FJ], dr[FJ];                  // this lane's output pixel offset in the tile, per fragment
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+        const int d = wm * 64 + j * 16 + (lane & 15);
+        dq[j] = d / g.OW;
+        dr[j] = d - dq[j] * g.OW;
+    }
+    const int p0 = wave * 8 + (lane >> 3);       // first patch pixel this lane DMAs
+    const int rr0 = p0 / WP, col0 = p0 - rr0 * WP;
+    const int qstep = 64 / WP, rstep = 64 - qstep * WP;  // pieces advance by 64 patch pixels
+
+    auto issue = [&](int tile, int buf) {
+        const int m0 = tile * kHaloBM;
+        int n = m0 / OHW;
+        int prel = (m0 - n * OHW) / g.OW + rr0;         // padded row (relative to image n) of p
+        int col = col0;
+        while (prel >= HP) {
+            prel -= HP;
+            ++n;
+        }
+        unsigned char* L = smem + buf * patch_bytes;
+        for (int piece = wave; piece * 8 < hg.patch_px; piece += 8) {
+            const int p = piece * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((p >> 1) & 7);     // source chunk of this lane's slot
+            const int ih = prel - 1, iw = col - 1;
+            const bool ok = p < hg.patch_px && n < g.N && (unsigned)ih < (unsigned)g.H &&
+                            (unsigned)iw < (unsigned)g.W;
+            const uint32_t off = ((uint32_t)((n * g.H + ih) * g.W + iw) * 64u + (uint32_t)c * 8u) * 2u;
+            dma16(xr, L + piece * 1024, ok ? off : 0x80000000u, 0);
+            col += rstep;
+            prel += qstep;
+            if (col >= WP) {
+                col -= WP;
+                ++prel;
+            }
+            while (prel >= HP) {
+                prel -= HP;
+                ++n;
+            }
+        }
+    };
+
+    issue(t0, 0);
+    int buf = 0;
+    for (int t = t0; t < t1; ++t) {
+        // patch t landed; only the previous tile's epilogue stores (FI * FJ per lane) may still fly
+        wait_vmcnt<FI * FJ>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + 1 < t1) issue(t + 1, buf ^ 1);
+        const unsigned char* L = smem + buf * patch_bytes;
+        const int m0 = t * kHaloBM;
+        const int n0 = m0 / OHW, r0m = m0 - n0 * OHW, oh0 = r0m / g.OW, ow0 = r0m - oh0 * g.OW;
+        int pp[FJ];                                   // patch pixel of tap (0, 0) per fragment
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+            int ow = ow0 + dr[j], oh = oh0 + dq[j], dn = 0;
+            if (ow >= g.OW) {
+                ow -= g.OW;
+                ++oh;
+            }
+            while (oh >= g.OH) {
+                oh -= g.OH;
+                ++dn;
+            }
+            // rows past M read a finite patch row and are not stored
+            pp[j] = (dn * HP + oh - oh0) * WP + ow;
+            if (pp[j] + 2 * WP + 2 >= hg.patch_px) pp[j] = 0;
+        }
+        f32x4 acc[FI][FJ];
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+            for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int toff = (tap / 3) * WP + (tap % 3);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int kq = ks * 4 + (lane >> 4);
+                bf16x8 xf[FJ];
+#pragma unroll
+                for (int j = 0; j < FJ; ++j) xf[j] = *reinterpret_cast<const bf16x8*>(L + swz_lin(pp[j] + toff, kq));
+#pragma unroll
+                for (int i = 0; i < FI; ++i)
+#pragma unroll
+                    for (int j = 0; j < FJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tap * 2 + ks][i], xf[j], acc[i][j], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+            const int m = m0 + wm * 64 + j * 16 + (lane & 15);
+            if (m >= g.M) continue;
+            __bf16* dst = g.y + (size_t)m * 64 + wn * 32 + 4 * (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < FI; ++i) {
+                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                bf16x4 o;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) o[v] = (__bf16)acc[i][j][v];
+                *reinterpret_cast<bf16x4*>(dst + i * 16) = o;
+            }
+        }
+        buf ^= 1;
+    }
+}
+
+// launches the halo kernel when the layer and the LDS budget allow; returns 1 when it does not
+int launch_conv3x3c64(const ConvGeom& g0, hipStream_t s) {
+    if (g0.Cin != 64 || g0.Cout != 64 || g0.KH != 3 || g0.KW != 3 || g0.stride != 1 || g0.pad != 1) return 1;
+    HaloGeom hg;
+    hg.g = g0;
+    hg.WP = g0.W + 2;
+    // output rows a 256-pixel tile can span, + 2 halo rows, + 2 pad rows per image boundary crossed
+    const int rows = (kHaloBM - 1 + g0.OW - 1) / g0.OW + 1;
+    const int imgs = (kHaloBM - 1 + g0.OH * g0.OW - 1) / (g0.OH * g0.OW) + 1;
+    hg.NR = rows + 2 + 2 * (imgs - 1);
+    hg.patch_px = (hg.NR * hg.WP + 7) / 8 * 8;      // whole 8-pixel DMA pieces
+    const size_t lds = (size_t)2 * hg.patch_px * kRowBytes;
+    if (lds > 160 * 1024) return 1;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3c64_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    const long long tiles = ((long long)g0.M + kHaloBM - 1) / kHaloBM;
+    hg.g.tiles = (int)tiles;
+    const int grid = (int)(tiles < cu_count() ? tiles : cu_count());
+    hipLaunchKernelGGL(conv3x3c64_kernel, dim3((unsigned)grid), dim3(kDmaThreads), lds, s, hg);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "conv3x3c64_kernel launch");
 }
 
 // weights [Cout, Cin, KH, KW] (fp32 or bf16) -> [Cout, KH, KW, Cin] bf16
@@ -270,18 +679,22 @@ int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream) {
     g.KT = g.KH * g.KW * g.cin_tiles;
     g.x_bytes = (uint32_t)((long long)g.N * g.H * g.W * g.Cin * 2);
     g.w_bytes = (uint32_t)((long long)g.Cout * g.KH * g.KW * g.Cin * 2);
-    const int BN = g.Cout % 128 == 0 ? 128 : 64;
-    g.tiles_n = g.Cout / BN;
-    const long long tiles = (long long)((g.M + kBM - 1) / kBM) * g.tiles_n;
-    if (tiles >= (1ll << 31)) return fail(MCGMIL_E_UNSUPPORTED, "too many tiles");
-    g.tiles = (int)tiles;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (BN == 128)
-        hipLaunchKernelGGL(conv_kernel<128>, dim3((unsigned)tiles), dim3(kConvThreads), 0, s, g);
-    else
-        hipLaunchKernelGGL(conv_kernel<64>, dim3((unsigned)tiles), dim3(kConvThreads), 0, s, g);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "conv_kernel launch");
+    // tile shape: 128 x 128 when Cout allows, else 256 x 64 (the same 64 x 64 block per wave);
+    // MCGMIL_CONV_TILE=128x64|256x64|128x128|dma256x64|dma512x64|dma256x128x2 forces one (A/B)
+    const char* force = getenv("MCGMIL_CONV_TILE");
+    if (force && !strcmp(force, "128x64")) return launch_conv<128, 64, 2>(g, s);
+    if (force && !strcmp(force, "256x64")) return launch_conv<256, 64, 4>(g, s);
+    if (force && !strcmp(force, "128x128") && g.Cout % 128 == 0) return launch_conv<128, 128, 2>(g, s);
+    if (force && !strcmp(force, "dma256x64")) return launch_conv_dma<256, 64, 4, 3>(g, s);
+    if (!(force && !strcmp(force, "nohalo"))) {
+        const int rc = launch_conv3x3c64(g, s);
+        if (rc != 1) return rc;
+    }
+    if (force && !strcmp(force, "dma512x64")) return launch_conv_dma<512, 64, 8, 2>(g, s);
+    if (force && !strcmp(force, "dma256x128x2") && g.Cout % 128 == 0) return launch_conv_dma<256, 128, 4, 2>(g, s);
+    if (g.Cout % 128 == 0) return launch_conv_dma<256, 128, 4, 3>(g, s);
+    return launch_conv_dma<256, 64, 4, 3>(g, s);
 }
 
 }  // extern "C"

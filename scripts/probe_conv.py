@@ -43,6 +43,11 @@ def main():
         oh = (h + 2 * p - k) // s + 1
         flop = 2.0 * K * oh * oh * cout * cin * k * k
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            tiles = {}
+            for tile in [t for t in os.environ.get("PROBE_TILES", "").split(",") if t]:
+                os.environ["MCGMIL_CONV_TILE"] = tile
+                tiles[tile] = round(flop / timed(lambda: conv2d(conv, x)) / 1e9, 1)
+            os.environ.pop("MCGMIL_CONV_TILE", None)
             own = timed(lambda: conv2d(conv, x))
             ref = timed(lambda: conv(x))
             y, yr = conv2d(conv, x), conv(x)
@@ -52,7 +57,8 @@ def main():
         print(json.dumps({"cin": cin, "hw": h, "cout": cout, "k": k, "stride": s, "count": count,
                           "own_ms": round(own, 4), "torch_ms": round(ref, 4),
                           "own_tflops": round(flop / own / 1e9, 1),
-                          "torch_tflops": round(flop / ref / 1e9, 1), "nrel_vs_torch": dev_rel}),
+                          "torch_tflops": round(flop / ref / 1e9, 1), "nrel_vs_torch": dev_rel,
+                          "forced_tile_tflops": tiles}),
               flush=True)
     print(json.dumps({"resnet18_block_convs_ms": {"own": round(tot_own, 3), "torch": round(tot_torch, 3)}}))
 

@@ -28,6 +28,12 @@ SHAPES = [
     (5, 64, 9, 11, 192, 3, 1, 1),
     (2, 128, 10, 10, 64, 5, 1, 2),
     (1, 64, 8, 13, 64, 7, 3, 3),
+    # 3x3 / 64 -> 64 halo-tile kernel: tiles spanning several small images, odd widths, a tile
+    # crossing image boundaries, and a width whose patch only just fits (62) or does not (70)
+    (9, 64, 8, 6, 64, 3, 1, 1),
+    (3, 64, 30, 17, 64, 3, 1, 1),
+    (2, 64, 20, 62, 64, 3, 1, 1),
+    (1, 64, 5, 70, 64, 3, 1, 1),
 ]
 
 
