@@ -23,7 +23,7 @@
  * C a multiple of 8, rows >= 1, x / residual / y 16-byte aligned.
  *
  * Semantics (torch.nn.functional.batch_norm + relu):
- *   batch statistics (mean == var == NULL): mean_c = (1/rows) sum x[:, c],
+ *   batch statistics (running_mean == running_var == NULL): mean_c = (1/rows) sum x[:, c],
  *     var_c = (1/rows) sum (x[:, c] - mean_c)^2 (biased, as torch normalises in training mode),
  *     accumulated in fp32 per workgroup around a per-channel shift (x[0, c]) and combined in fp64;
  *   running statistics (both given): mean_c, var_c as passed;
@@ -66,11 +66,14 @@ typedef struct mcgmil_bn_args {
     int32_t pool_kernel;        /* 0: none; k > 0: max-pool k x k after the activation */
     int32_t pool_stride, pool_pad;  /* torch MaxPool2d(k, stride, pad): -inf padding, floor mode;
                                        y is then [N * Ho * Wo, C], Ho = (H + 2 pad - k) / stride + 1 */
-    int32_t reserved;
+    int32_t num_partials;       /* rows of `partials` (0: none) */
     float* batch_mean;          /* optional out [C]: the mean used */
     float* batch_invstd;        /* optional out [C]: 1 / sqrt(var + eps) */
     void* workspace;            /* >= mcgmil_bn_workspace_size() bytes, 256-byte aligned */
     size_t workspace_bytes;
+    const float* partials;      /* optional [num_partials][3][C] (count, mean, M2) blocks of x, as
+                                   mcgmil_conv2d's stats: batch statistics from them (Chan's
+                                   combination in fp64, fixed order) instead of a pass over x */
 } mcgmil_bn_args;
 
 size_t mcgmil_bn_args_size(void);   /* sizeof(mcgmil_bn_args), for binding checks */
@@ -89,6 +92,12 @@ typedef struct mcgmil_conv_args {
     const void* x;              /* bf16 [batch, height, width, in_channels] */
     const void* w;              /* packed bf16 [out_channels, kernel_h, kernel_w, in_channels] */
     void* y;                    /* bf16 [batch, OH, OW, out_channels] */
+    float* stats;               /* optional out: BatchNorm statistics of y, [parts][3][out_channels]
+                                   = (count, mean, M2) of the bf16 outputs per workgroup row,
+                                   parts = mcgmil_conv_stats_parts() (0 when the layer's
+                                   kernel emits none: then stats is ignored and the BN computes
+                                   its statistics from y); hand them to mcgmil_batchnorm_act as
+                                   partials. NULL: not computed */
 } mcgmil_conv_args;
 
 size_t mcgmil_conv_args_size(void);
@@ -133,6 +142,7 @@ int mcgmil_pack_stem_weights(const mcgmil_stem_args* a, const void* weight, int3
                              void* packed, void* stream);
 int mcgmil_stem_workspace_size(const mcgmil_stem_args* a, size_t* bytes);
 int mcgmil_stem_forward(const mcgmil_stem_args* a, void* stream);
+int mcgmil_conv_stats_parts(const mcgmil_conv_args* a, int32_t* parts);
 int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream);
 int mcgmil_bn_workspace_size(const mcgmil_bn_args* a, size_t* bytes);
 int mcgmil_batchnorm_act(const mcgmil_bn_args* a, void* stream);

@@ -114,6 +114,18 @@ __global__ __launch_bounds__(kThreads) void bn_partial_kernel(const E* __restric
     }
 }
 
+// a_c = gamma_c / sqrt(var_c + eps), b_c = beta_c - mean_c a_c (fp64, stored fp32)
+__device__ __forceinline__ void write_ab(int c, int C, double mean, double var, const float* gamma,
+                                         const float* beta, double eps, float* ab, float* bmean,
+                                         float* binvstd) {
+    const double inv = 1.0 / sqrt(var + eps);
+    const double g = gamma ? (double)gamma[c] : 1.0, bt = beta ? (double)beta[c] : 0.0;
+    ab[c] = (float)(g * inv);
+    ab[C + c] = (float)(bt - mean * g * inv);
+    if (bmean) bmean[c] = (float)mean;
+    if (binvstd) binvstd[c] = (float)inv;
+}
+
 // One workgroup per 8 channels, 32 lanes per channel each summing every 32nd partial in fp64;
 // the 32 lane sums are combined in lane order (deterministic for a given partial count).
 template <typename E>
@@ -128,6 +140,8 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(const float* __re
     const int c = blockIdx.x * kFinCh + cl;
     double S = 0.0, SS = 0.0;
     if (!rmean && c < C) {
+        // unrolled so the partial loads are all in flight (same summation order: one chain each)
+#pragma unroll 8
         for (int b = lane; b < parts; b += kFinLanes) {
             S += (double)part[((size_t)b * 2) * C + c];
             SS += (double)part[((size_t)b * 2 + 1) * C + c];
@@ -154,12 +168,47 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(const float* __re
         if (var < 0.0) var = 0.0;
         mean = (double)sh[c & 7] + m;
     }
-    const double inv = 1.0 / sqrt(var + eps);
-    const double g = gamma ? (double)gamma[c] : 1.0, bt = beta ? (double)beta[c] : 0.0;
-    ab[c] = (float)(g * inv);
-    ab[C + c] = (float)(bt - mean * g * inv);
-    if (bmean) bmean[c] = (float)mean;
-    if (binvstd) binvstd[c] = (float)inv;
+    write_ab(c, C, mean, var, gamma, beta, eps, ab, bmean, binvstd);
+}
+
+// Statistics from (count, mean, M2) blocks [parts][3][C] (mcgmil_conv2d's epilogue). In fp64,
+// around the channel's first block mean m0: N = sum n_b, S = sum n_b (m_b - m0),
+// Q = sum M2_b + n_b (m_b - m0)^2, so mean = m0 + S / N and var = (Q - S^2 / N) / N -- exact
+// Chan combination without a division per block. Each of 32 lanes sums every 32nd block, then
+// the lanes in order (deterministic).
+__global__ __launch_bounds__(kThreads) void bn_finalize_chan_kernel(const float* __restrict__ part, int parts,
+                                                                  int C, const float* gamma, const float* beta,
+                                                                  double eps, float* __restrict__ ab,
+                                                                  float* bmean, float* binvstd) {
+    __shared__ double red[3][kThreads];
+    const int tid = threadIdx.x, lane = tid / kFinCh, cl = tid % kFinCh;
+    const int c = blockIdx.x * kFinCh + cl;
+    double n = 0.0, S = 0.0, Q = 0.0, m0 = 0.0;
+    if (c < C) {
+        m0 = (double)part[C + c];
+#pragma unroll 8
+        for (int b = lane; b < parts; b += kFinLanes) {
+            const double nb = (double)part[((size_t)b * 3) * C + c];
+            const double d = (double)part[((size_t)b * 3 + 1) * C + c] - m0;
+            n += nb;
+            S = fma(nb, d, S);
+            Q += fma(nb * d, d, (double)part[((size_t)b * 3 + 2) * C + c]);
+        }
+    }
+    red[0][tid] = n;
+    red[1][tid] = S;
+    red[2][tid] = Q;
+    __syncthreads();
+    if (lane != 0 || c >= C) return;
+    for (int k = 1; k < kFinLanes; ++k) {
+        n += red[0][k * kFinCh + cl];
+        S += red[1][k * kFinCh + cl];
+        Q += red[2][k * kFinCh + cl];
+    }
+    const double mean = n > 0.0 ? m0 + S / n : 0.0;
+    double var = n > 0.0 ? (Q - S * S / n) / n : 0.0;
+    if (var < 0.0) var = 0.0;
+    write_ab(c, C, mean, var, gamma, beta, eps, ab, bmean, binvstd);
 }
 
 // Grid-stride over 8-channel vectors; the total thread count is a multiple of C/8, so every
@@ -289,6 +338,8 @@ int validate(const mcgmil_bn_args* a) {
         return fail(MCGMIL_E_INVALID, "running_mean and running_var go together");
     if (!(a->eps >= 0.0)) return fail(MCGMIL_E_INVALID, "eps must be >= 0");
     if (a->relu != 0 && a->relu != 1) return fail(MCGMIL_E_INVALID, "relu must be 0 or 1");
+    if (a->partials && (a->num_partials < 1 || ((uintptr_t)a->partials & 3)))
+        return fail(MCGMIL_E_INVALID, "partials need num_partials >= 1 and 4-byte alignment");
     if (a->pool_kernel < 0) return fail(MCGMIL_E_INVALID, "pool_kernel must be >= 0");
     if (a->pool_kernel > 0) {
         if (a->batch < 1 || a->height < 1 || a->width < 1 ||
@@ -320,13 +371,10 @@ void launch_apply(const mcgmil_bn_args* a, const float* ab, hipStream_t s) {
 
 // finalize (statistics from `parts` partial sums around the per-channel shift row `shift`, or
 // the running statistics) then the normalise / pool pass; ab lives at the workspace start
+// the normalise / pool pass with a, b at ab
 template <typename E>
-int finish(const mcgmil_bn_args* a, const float* part, int parts, const E* shift, hipStream_t s) {
+int apply_step(const mcgmil_bn_args* a, const float* ab, hipStream_t s) {
     const int C = a->channels;
-    float* ab = static_cast<float*>(a->workspace);   // [2][C]
-    hipLaunchKernelGGL(bn_finalize_kernel<E>, dim3((C + kFinCh - 1) / kFinCh), dim3(kThreads), 0, s, part, parts, a->rows,
-                       C, shift, a->gamma, a->beta, a->running_mean, a->running_var, a->eps, ab,
-                       a->batch_mean, a->batch_invstd);
     if (a->pool_kernel > 0) {
         const int Ho = pooled_dim(a->height, a), Wo = pooled_dim(a->width, a);
         const long long nvec = (long long)a->batch * Ho * Wo * (C / 8);
@@ -353,11 +401,30 @@ int finish(const mcgmil_bn_args* a, const float* part, int parts, const E* shift
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "batchnorm launch");
 }
 
+// finalize (statistics from `parts` partial sums around the per-channel shift row `shift`, or
+// the running statistics) then the normalise / pool pass; ab lives at the workspace start
+template <typename E>
+int finish(const mcgmil_bn_args* a, const float* part, int parts, const E* shift, hipStream_t s) {
+    const int C = a->channels;
+    float* ab = static_cast<float*>(a->workspace);   // [2][C]
+    hipLaunchKernelGGL(bn_finalize_kernel<E>, dim3((C + kFinCh - 1) / kFinCh), dim3(kThreads), 0, s, part, parts, a->rows,
+                       C, shift, a->gamma, a->beta, a->running_mean, a->running_var, a->eps, ab,
+                       a->batch_mean, a->batch_invstd);
+    return apply_step<E>(a, ab, s);
+}
+
 template <typename E>
 int run(const mcgmil_bn_args* a, hipStream_t s) {
     const int C = a->channels;
     float* part = static_cast<float*>(a->workspace) + 2 * C;   // [parts][2][C]
     const E* x = static_cast<const E*>(a->x);
+    if (!a->running_mean && a->partials) {       // statistics from the producer's (n, mean, M2)
+        float* ab = static_cast<float*>(a->workspace);
+        hipLaunchKernelGGL(bn_finalize_chan_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kThreads), 0, s,
+                           a->partials, a->num_partials, C, a->gamma, a->beta, a->eps, ab, a->batch_mean,
+                           a->batch_invstd);
+        return apply_step<E>(a, ab, s);
+    }
     int parts = 0;
     if (!a->running_mean) {
         parts = parts_for(a);

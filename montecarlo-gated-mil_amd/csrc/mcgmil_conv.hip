@@ -6,24 +6,37 @@
 //   C[m, co] = sum_k A[m, k] * B[k, co],  m = (n, oh, ow),  k = (kh, kw, ci)
 //   A[m, k]  = x[n, oh*s - pad + kh, ow*s - pad + kw, ci]   (0 outside the image)
 //   B[k, co] = w[co, kh, kw, ci]                            (weights packed channels-last)
-// One 256-thread workgroup computes a 128-pixel x BN-channel tile (BN = 128, or 64 when the
-// layer has 64 output channels) over K tiles of 64: each K tile is one (kh, kw) position and 64
-// consecutive input channels, so every A row of a K tile is ONE contiguous 128-byte run of the
-// NHWC input (a 16-byte buffer load per lane, zero-filled by the descriptor's range check where
-// the window leaves the image). Tiles are staged through LDS (double buffered, XOR-swizzled
-// 128-byte rows, register staging, one barrier per K tile); 4 waves in a 2 x 2 grid each own a
-// 64-pixel x BN/2-channel block of v_mfma_f32_16x16x32_bf16 accumulators (weights as the A
-// operand, so a lane ends with 4 consecutive channels of one pixel: one 8-byte store each).
-// fp32 accumulation, one rounding to bf16 -- the same arithmetic as MIOpen's bf16 convolution
-// under torch.autocast, up to the summation order.
+// A K tile is one (kh, kw) tap and 64 consecutive input channels, so every A row of a K tile is
+// ONE contiguous 128-byte run of the NHWC input. v_mfma_f32_16x16x32_bf16 with the weights as
+// the A operand: a lane ends with 4 consecutive channels of one pixel (one 8-byte store each).
+// fp32 accumulation, one rounding to bf16 -- the arithmetic of MIOpen's bf16 convolution under
+// torch.autocast, up to the summation order.
+//
+// Two kernels, both persistent (one 8-wave workgroup per CU) and fed by LDS-DMA
+// (buffer_load_dwordx4 ... lds: no staging registers, no ds_write pass; out-of-image taps use an
+// out-of-range offset, which the descriptor's range check turns into zeros):
+//   conv_dma_kernel    any layer: 256 pixels x BN channels per tile, three LDS stages, the
+//                      (tile, K tile) steps of a workgroup streamed with a counted vmcnt and raw
+//                      barriers; every workgroup keeps one channel tile (so its lanes' channels
+//                      never change) and walks a contiguous range of pixel tiles.
+//   conv3x3c64_kernel  3x3 / stride 1 / 64 -> 64 (ResNet layer 1): weights resident in
+//                      registers, each tile's input rows DMA'd once into a zero-padded LDS patch
+//                      that all 9 taps read (the generic kernel fetches every pixel 9 times and
+//                      is L2-bound on these layers).
+// Optional BatchNorm statistics (a->stats, conv_dma_kernel only): each lane keeps running sums of its channels' bf16
+// outputs around its first value; at the end the lanes and waves of a workgroup are merged
+// (Chan's pairwise update, fixed order) into one (count, mean, M2) block per workgroup, which
+// mcgmil_batchnorm_act combines in fp64 -- the activation is then never re-read for statistics.
 #include <hip/hip_runtime.h>
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <type_traits>
 
 #include "../../include/mcgmil_features.h"
 #include "mcgmil_device.h"
@@ -35,21 +48,24 @@ using namespace mcgmil;
 using mcgmil_detail::fail;
 using mcgmil_detail::hip_fail;
 
-constexpr int kConvThreads = 256;
-constexpr int kBM = 256;            // largest pixel tile (host-side size check)
+constexpr int kThreads = 512;       // 8 waves
+constexpr int kBM = 256;            // output pixels per tile
 constexpr int kBK = 64;             // K elements per stage (one 128-byte row per pixel/channel)
 constexpr int kRowBytes = kBK * 2;
+constexpr int kStages = 3;
 
 struct ConvGeom {
     const __bf16* x;
     const __bf16* w;
     __bf16* y;
+    float* stats;        // [Gm][3][Cout] (count, mean, M2) per workgroup row, or NULL
     int N, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad;
     int M;               // N * OH * OW (< 2^31, host-checked)
     int KT;              // K tiles: KH * KW * Cin / 64
     int cin_tiles;       // Cin / 64
-    int tiles_n;         // Cout / BN
-    int tiles;           // tiles_m * tiles_n
+    int tiles_m;         // pixel tiles
+    int tiles_n;         // channel tiles: Cout / BN
+    int Gm;              // workgroups per channel tile
     uint32_t x_bytes;    // buffer range of x (< 2^31, host-checked)
     uint32_t w_bytes;
 };
@@ -61,162 +77,10 @@ __device__ __forceinline__ uint32_t swz(int r, int c) {
     return (uint32_t)r * kRowBytes + (uint32_t)((c ^ ((r >> 1) & 7)) << 4);
 }
 
-// XCD-aware tile order (guide T1, bijective form): consecutive logical tiles -- the BN-column
-// tiles of one pixel tile, which read the same input rows -- land on the same XCD's L2.
+// XCD-aware order (guide T1, bijective form): consecutive logical ids land on one XCD's L2
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-}
-
-// BM pixels x BN channels per workgroup; the 4 waves form a WGM x (4 / WGM) grid, each owning
-// BM / WGM pixels x BN / (4 / WGM) channels (64 x 64 for the 128 x 128 and 256 x 64 shapes).
-template <int BM, int BN, int WGM>
-__global__ __launch_bounds__(kConvThreads, 2) void conv_kernel(const ConvGeom g) {
-    constexpr int WGN = 4 / WGM;
-    constexpr int STAGE = (BM + BN) * kRowBytes;      // A rows then B rows
-    constexpr int NA = BM / 32;                       // A chunks per thread per stage
-    constexpr int NB = BN / 32;                       // B chunks per thread per stage
-    constexpr int WM = BM / WGM, WN = BN / WGN;       // wave tile
-    constexpr int FI = WN / 16;                       // channel fragments per wave
-    constexpr int FJ = WM / 16;                       // pixel fragments per wave
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int t = xcd_remap((int)blockIdx.x, (int)gridDim.x);
-    if (t >= g.tiles) return;
-    const int tm = t / g.tiles_n, tn = t - tm * g.tiles_n;
-    const int m0 = tm * BM, n0 = tn * BN;
-
-    // ---- staging assignment: chunk c of rows (tid >> 3) + 32 i
-    const int c = tid & 7, r0 = tid >> 3;
-    const __amdgpu_buffer_rsrc_t xr = make_rsrc(g.x, g.x_bytes);
-    const __amdgpu_buffer_rsrc_t wr = make_rsrc(g.w, g.w_bytes);
-    int pix_base[NA], ih0[NA], iw0[NA];
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-        const int m = m0 + r0 + 32 * i;
-        const int mm = m < g.M ? m : 0;
-        const int n = mm / (g.OH * g.OW);
-        const int rem = mm - n * g.OH * g.OW;
-        const int oh = rem / g.OW, ow = rem - (rem / g.OW) * g.OW;
-        pix_base[i] = n * g.H * g.W;
-        // rows past M get a window that never fits, so they load zeros
-        ih0[i] = m < g.M ? oh * g.stride - g.pad : -(1 << 28);
-        iw0[i] = ow * g.stride - g.pad;
-    }
-    const uint32_t K = (uint32_t)(g.KH * g.KW * g.Cin);
-    uint32_t wrow[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) wrow[i] = ((uint32_t)(n0 + r0 + 32 * i) * K + (uint32_t)c * 8u) * 2u;
-
-    uint4 ra[NA], rb[NB];
-    auto load = [&](int kt) {
-        const int khw = kt / g.cin_tiles, cc = kt - khw * g.cin_tiles;
-        const int kh = khw / g.KW, kw = khw - kh * g.KW;
-#pragma unroll
-        for (int i = 0; i < NA; ++i) {
-            const int ih = ih0[i] + kh, iw = iw0[i] + kw;
-            const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-            const uint32_t off = ((uint32_t)(pix_base[i] + ih * g.W + iw) * (uint32_t)g.Cin +
-                                  (uint32_t)(cc * 64 + c * 8)) * 2u;
-            ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  xr, ok ? off : 0x80000000u, 0, 0));
-        }
-#pragma unroll
-        for (int i = 0; i < NB; ++i)
-            rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  wr, wrow[i], (uint32_t)kt * (kBK * 2u), 0));
-    };
-    auto store = [&](int buf) {
-        unsigned char* A = smem + buf * STAGE;
-        unsigned char* B = A + BM * kRowBytes;
-#pragma unroll
-        for (int i = 0; i < NA; ++i) *reinterpret_cast<uint4*>(A + swz(r0 + 32 * i, c)) = ra[i];
-#pragma unroll
-        for (int i = 0; i < NB; ++i) *reinterpret_cast<uint4*>(B + swz(r0 + 32 * i, c)) = rb[i];
-    };
-
-    // ---- compute assignment: wave (wm, wn) owns pixels wm*WM.. and channels wn*WN..
-    const int wm = wave / WGN, wn = wave % WGN;
-    f32x4 acc[FI][FJ];
-#pragma unroll
-    for (int i = 0; i < FI; ++i)
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    auto compute = [&](int buf) {
-        const unsigned char* A = smem + buf * STAGE;
-        const unsigned char* B = A + BM * kRowBytes;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const int kq = ks * 4 + (lane >> 4);
-            bf16x8 wf[FI], xf[FJ];
-#pragma unroll
-            for (int i = 0; i < FI; ++i)
-                wf[i] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WN + i * 16 + (lane & 15), kq));
-#pragma unroll
-            for (int j = 0; j < FJ; ++j)
-                xf[j] = *reinterpret_cast<const bf16x8*>(A + swz(wm * WM + j * 16 + (lane & 15), kq));
-#pragma unroll
-            for (int i = 0; i < FI; ++i)
-#pragma unroll
-                for (int j = 0; j < FJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
-        }
-    };
-
-    load(0);
-    store(0);
-    __syncthreads();
-    for (int kt = 0; kt < g.KT; ++kt) {
-        const bool more = kt + 1 < g.KT;
-        if (more) load(kt + 1);
-        compute(kt & 1);
-        if (more) store((kt + 1) & 1);
-        __syncthreads();
-    }
-
-    // ---- epilogue: lane holds channels 4*(lane>>4)+v of pixel (lane & 15) per fragment
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-        const int m = m0 + wm * WM + j * 16 + (lane & 15);
-        if (m >= g.M) continue;
-        __bf16* dst = g.y + (size_t)m * g.Cout + n0 + wn * WN + 4 * (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < FI; ++i) {
-            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-            bf16x4 o;
-#pragma unroll
-            for (int v = 0; v < 4; ++v) o[v] = (__bf16)acc[i][j][v];
-            *reinterpret_cast<bf16x4*>(dst + i * 16) = o;
-        }
-    }
-}
-
-// ---- LDS-DMA variant: 8 waves, BM x BN tiles, three LDS stages filled by buffer_load ... lds
-// (no staging registers, no ds_write pass). Each wave-instruction moves 1 KiB = 8 rows of 128 B
-// straight into LDS (lane L: row L / 8, slot L % 8); the XOR swizzle goes on the SOURCE chunk
-// (slot s of row r holds chunk s ^ ((r >> 1) & 7)), so the fragment reads are the same swz() as
-// above. Out-of-image taps use an out-of-range offset: the descriptor's range check returns 0.
-// One persistent workgroup per CU walks its tiles' (tile, K tile) steps as one stream: step s + 2 is
-// issued right after the barrier that opens step s (so each DMA has two compute phases to land, and
-// the next tile's first stages load under this tile's last steps and epilogue); the wait is a
-// counted vmcnt (the other stage stays in flight) before a raw s_barrier (a __syncthreads would
-// drain both).
-constexpr int kDmaThreads = 512;
-
-int cu_count() {
-    static std::atomic<int> cache[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
-    if (dev < 64) {
-        const int c = cache[dev].load(std::memory_order_relaxed);
-        if (c > 0) return c;
-    }
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-    if (dev < 64) cache[dev].store(cus, std::memory_order_relaxed);
-    return cus;
 }
 
 // 16 bytes per lane from a buffer straight into LDS at the wave-uniform base + 16 * lane. The
@@ -235,9 +99,131 @@ __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int WGM, int NS>
-__global__ __launch_bounds__(kDmaThreads, 1) void conv_dma_kernel(const ConvGeom g) {
-    constexpr int WGN = 8 / WGM;
+int cu_count() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+    if (dev < 64) {
+        const int c = cache[dev].load(std::memory_order_relaxed);
+        if (c > 0) return c;
+    }
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    if (dev < 64) cache[dev].store(cus, std::memory_order_relaxed);
+    return cus;
+}
+
+// ---- BatchNorm statistics of the output (see the header comment)
+// Running sums of NCH channels of one lane: around x0 (the lane's first value per channel).
+template <int NCH>
+struct LaneStats {
+    float x0[NCH], S[NCH], SS[NCH];
+    float n;
+};
+
+// (n, m, M2) <- merge with (nb, mb, M2b) for every channel (the counts are shared by the channels)
+template <int NCH>
+__device__ __forceinline__ void chan_merge(float& n, float (&m)[NCH], float (&M2)[NCH], float nb,
+                                           const float (&mb)[NCH], const float (&M2b)[NCH]) {
+    const float nn = n + nb;
+    const float f = nn > 0.f ? nb / nn : 0.f, h = n * f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const float d = mb[c] - m[c];
+        m[c] = fmaf(d, f, m[c]);
+        M2[c] = M2[c] + M2b[c] + d * d * h;
+    }
+    n = nn;
+}
+
+// End of kernel: lanes -> (n, mean, M2); merged over the 16 pixel lanes of each channel group
+// (butterfly, the lane-0 result kept), then over the WGM waves that share channels (LDS, wave
+// order). Lane channel of index c = 4 i + v: chan0 + 16 i + 4 (lane >> 4) + v (local to the
+// workgroup's channel tile of width BN). Writes stats[(row * 3 + k) * Cout + col0 + local].
+template <int NCH, int WGM, int BN>
+__device__ void write_stats(const LaneStats<NCH>& st, int chan0, int wm, float* lds, float* stats,
+                            int row, int Cout, int col0) {
+    const int lane = threadIdx.x & 63;
+    float n = st.n, m[NCH], M2[NCH];
+    const float rn = n > 0.f ? 1.f / n : 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        m[c] = st.x0[c] + st.S[c] * rn;
+        M2[c] = fmaxf(st.SS[c] - st.S[c] * st.S[c] * rn, 0.f);
+        if (!(n > 0.f)) m[c] = M2[c] = 0.f;
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+        float mb[NCH], M2b[NCH];
+        const float nb = __shfl_xor(n, o, 64);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            mb[c] = __shfl_xor(m[c], o, 64);
+            M2b[c] = __shfl_xor(M2[c], o, 64);
+        }
+        chan_merge<NCH>(n, m, M2, nb, mb, M2b);
+    }
+    __syncthreads();                                   // LDS stages no longer read
+    float* red = lds;                                  // [WGM][3][BN]
+    if ((lane & 15) == 0) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int local = chan0 + 16 * (c >> 2) + 4 * (lane >> 4) + (c & 3);
+            red[(wm * 3 + 0) * BN + local] = n;
+            red[(wm * 3 + 1) * BN + local] = m[c];
+            red[(wm * 3 + 2) * BN + local] = M2[c];
+        }
+    }
+    __syncthreads();
+    for (int local = threadIdx.x; local < BN; local += blockDim.x) {
+        float cn = red[local], cm[1] = {red[BN + local]}, cM2[1] = {red[2 * BN + local]};
+        for (int w = 1; w < WGM; ++w) {
+            const float mb[1] = {red[(w * 3 + 1) * BN + local]}, M2b[1] = {red[(w * 3 + 2) * BN + local]};
+            chan_merge<1>(cn, cm, cM2, red[(w * 3) * BN + local], mb, M2b);
+        }
+        stats[((size_t)row * 3 + 0) * Cout + col0 + local] = cn;
+        stats[((size_t)row * 3 + 1) * Cout + col0 + local] = cm[0];
+        stats[((size_t)row * 3 + 2) * Cout + col0 + local] = cM2[0];
+    }
+}
+
+// The epilogue of one pixel fragment: round to bf16, store 4 x 8 bytes, accumulate statistics.
+// PRED: pixels past M are neither stored nor counted (only the last tile can have them).
+template <int FI, bool STATS, bool PRED>
+__device__ __forceinline__ void store_fragment(const f32x4 (&acc)[FI], __bf16* dst, bool valid,
+                                               bool first, LaneStats<4 * FI>& st) {
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+        bf16x4 o;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) o[v] = (__bf16)acc[i][v];
+        if (!PRED || valid) *reinterpret_cast<bf16x4*>(dst + i * 16) = o;
+        if (STATS) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const float x = (float)o[v];
+                if (first) st.x0[4 * i + v] = x;
+                float d = x - st.x0[4 * i + v];
+                if (PRED) d = valid ? d : 0.f;
+                st.S[4 * i + v] += d;
+                st.SS[4 * i + v] = fmaf(d, d, st.SS[4 * i + v]);
+            }
+        }
+    }
+    if (STATS) st.n += (!PRED || valid) ? 1.f : 0.f;
+}
+
+// ---- conv_dma_kernel: 256 x BN tiles, 8 waves as 4 (pixels) x 2 (channels) for BN = 128 or
+// 4 x 2 of 64 x 32 for BN = 64. Workgroup (logical id L): channel tile tn = L % tiles_n and the
+// contiguous pixel tiles of row gm = L / tiles_n; ids of one row sit on one XCD (same input rows
+// in L2). Its (pixel tile, K tile) steps form one stream through three LDS stages: step s + 2 is
+// issued right after the barrier that opens step s (two compute phases to land; the next tile's
+// first stages load under this tile's last steps and epilogue); the wait is a counted vmcnt
+// before a raw s_barrier (a __syncthreads would drain the stage still in flight).
+template <int BN, bool STATS>
+__global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g) {
+    constexpr int BM = kBM, WGM = 4, WGN = 2;
     constexpr int STAGE = (BM + BN) * kRowBytes;
     constexpr int PA = BM / 64, PB = BN / 64;         // 1-KiB pieces per wave per stage (A, B)
     constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -245,23 +231,27 @@ __global__ __launch_bounds__(kDmaThreads, 1) void conv_dma_kernel(const ConvGeom
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // persistent: workgroup b owns the contiguous tiles [t0, t1) (consecutive tiles are the column
-    // tiles of one pixel tile: same input rows, same L2); the (tile, K tile) steps form one stream
-    const int t0 = (int)((long long)blockIdx.x * g.tiles / gridDim.x);
-    const int t1 = (int)((long long)(blockIdx.x + 1) * g.tiles / gridDim.x);
-    const int steps = (t1 - t0) * g.KT;
-    if (steps <= 0) return;
+    const int L = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int tn = L % g.tiles_n, gm = L / g.tiles_n;
+    const int tm0 = (int)((long long)gm * g.tiles_m / g.Gm);
+    const int tm1 = (int)((long long)(gm + 1) * g.tiles_m / g.Gm);
+    const int steps = (tm1 - tm0) * g.KT;
     const __amdgpu_buffer_rsrc_t xr = make_rsrc(g.x, g.x_bytes);
     const __amdgpu_buffer_rsrc_t wr = make_rsrc(g.w, g.w_bytes);
     const uint32_t K = (uint32_t)(g.KH * g.KW * g.Cin);
 
-    // issue side: the DMA addresses of the tile being fetched (runs two steps ahead of compute)
-    int itile = -1;
-    int pix_base[PA], ih0[PA], iw0[PA], cha[PA];
+    // B (weights) pieces: fixed channel tile
     uint32_t wrow[PB];
-    auto setup = [&](int tile) {
-        itile = tile;
-        const int tm = tile / g.tiles_n, tn = tile - tm * g.tiles_n;
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+        const int r = 8 * (wave + 8 * j) + (lane >> 3);
+        wrow[j] = ((uint32_t)(tn * BN + r) * K + (uint32_t)(((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
+    }
+    // A pieces: the pixel rows of the tile being fetched (the issue side runs two steps ahead)
+    int itm = -1;
+    int pix_base[PA], ih0[PA], iw0[PA], cha[PA];
+    auto setup = [&](int tm) {
+        itm = tm;
 #pragma unroll
         for (int j = 0; j < PA; ++j) {
             const int r = 8 * (wave + 8 * j) + (lane >> 3);
@@ -275,15 +265,10 @@ __global__ __launch_bounds__(kDmaThreads, 1) void conv_dma_kernel(const ConvGeom
             iw0[j] = ow * g.stride - g.pad;
             cha[j] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;     // source chunk of this lane's LDS slot
         }
-#pragma unroll
-        for (int j = 0; j < PB; ++j) {
-            const int r = 8 * (wave + 8 * j) + (lane >> 3);
-            wrow[j] = ((uint32_t)(tn * BN + r) * K + (uint32_t)(((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
-        }
     };
     auto issue = [&](int step, int buf) {
-        const int tile = t0 + step / g.KT, kt = step - (tile - t0) * g.KT;
-        if (tile != itile) setup(tile);
+        const int tm = tm0 + step / g.KT, kt = step - (tm - tm0) * g.KT;
+        if (tm != itm) setup(tm);
         const int khw = kt / g.cin_tiles, cc = kt - khw * g.cin_tiles;
         const int kh = khw / g.KW, kw = khw - kh * g.KW;
         unsigned char* A = smem + buf * STAGE;
@@ -302,11 +287,17 @@ __global__ __launch_bounds__(kDmaThreads, 1) void conv_dma_kernel(const ConvGeom
     };
 
     const int wm = wave / WGN, wn = wave % WGN;
-    f32x4 acc[FI][FJ];
+    f32x4 acc[FJ][FI];
 #pragma unroll
-    for (int i = 0; i < FI; ++i)
+    for (int j = 0; j < FJ; ++j)
 #pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < FI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    LaneStats<4 * FI> st;
+    if (STATS) {
+        st.n = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4 * FI; ++c) st.x0[c] = st.S[c] = st.SS[c] = 0.f;
+    }
 
     auto compute = [&](int buf) {
         const unsigned char* A = smem + buf * STAGE;
@@ -325,102 +316,52 @@ __global__ __launch_bounds__(kDmaThreads, 1) void conv_dma_kernel(const ConvGeom
             for (int i = 0; i < FI; ++i)
 #pragma unroll
                 for (int j = 0; j < FJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[j][i], 0, 0, 0);
         }
     };
-    // lane holds channels 4*(lane>>4)+v of pixel (lane & 15) per fragment
-    auto epilogue = [&](int tile) {
-        const int tm = tile / g.tiles_n, tn = tile - tm * g.tiles_n;
+    auto epilogue = [&](int tm, bool first) {
+        const bool full = (tm + 1) * BM <= g.M;
 #pragma unroll
         for (int j = 0; j < FJ; ++j) {
             const int m = tm * BM + wm * WM + j * 16 + (lane & 15);
-            if (m >= g.M) continue;
-            __bf16* dst = g.y + (size_t)m * g.Cout + tn * BN + wn * WN + 4 * (lane >> 4);
+            __bf16* dst = g.y + (size_t)(m < g.M ? m : 0) * g.Cout + tn * BN + wn * WN + 4 * (lane >> 4);
+            if (full) store_fragment<FI, STATS, false>(acc[j], dst, true, first && j == 0, st);
+            else store_fragment<FI, STATS, true>(acc[j], dst, m < g.M, first && j == 0, st);
 #pragma unroll
-            for (int i = 0; i < FI; ++i) {
-                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-                bf16x4 o;
-#pragma unroll
-                for (int v = 0; v < 4; ++v) o[v] = (__bf16)acc[i][j][v];
-                *reinterpret_cast<bf16x4*>(dst + i * 16) = o;
-            }
+            for (int i = 0; i < FI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-#pragma unroll
-        for (int i = 0; i < FI; ++i)
-#pragma unroll
-            for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
 
-    // NS LDS stages: step st + NS - 1 is issued into the stage step st - 1 used
-    issue(0, 0);
-    if (NS == 3 && steps > 1) issue(1, 1);
-    int buf = 0, kt = 0, tile = t0;
-    for (int st = 0; st < steps; ++st) {
-        // step st landed (counted: the next step's DMAs may stay in flight; vmcnt retires in order)
-        if (NS == 3 && st + 1 < steps) wait_vmcnt<PA + PB>();
+    if (steps > 0) {
+        issue(0, 0);
+        if (steps > 1) issue(1, 1);
+    }
+    int buf = 0, kt = 0, tm = tm0;
+    for (int s = 0; s < steps; ++s) {
+        // step s landed (counted: the next step's DMAs may stay in flight; vmcnt retires in order)
+        if (s + 1 < steps) wait_vmcnt<PA + PB>();
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (st + NS - 1 < steps) issue(st + NS - 1, buf == 0 ? NS - 1 : buf - 1);
+        if (s + 2 < steps) issue(s + 2, buf == 0 ? kStages - 1 : buf - 1);
         compute(buf);
-        buf = buf == NS - 1 ? 0 : buf + 1;
+        buf = buf == kStages - 1 ? 0 : buf + 1;
         if (++kt == g.KT) {
-            epilogue(tile);
+            epilogue(tm, tm == tm0);
             kt = 0;
-            ++tile;
+            ++tm;
         }
     }
-}
-
-template <int BM, int BN, int WGM, int NS>
-int launch_conv_dma(const ConvGeom& g0, hipStream_t s) {
-    static std::once_flag once;
-    auto k = conv_dma_kernel<BM, BN, WGM, NS>;
-    std::call_once(once, [&] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    });
-    ConvGeom g = g0;
-    g.tiles_n = g.Cout / BN;
-    const long long tiles = (long long)((g.M + BM - 1) / BM) * g.tiles_n;
-    if (tiles >= (1ll << 31)) return fail(MCGMIL_E_UNSUPPORTED, "too many tiles");
-    g.tiles = (int)tiles;
-    const size_t lds = (size_t)NS * (BM + BN) * kRowBytes;
-    const int grid = (int)(tiles < cu_count() ? tiles : cu_count());    // one workgroup per CU
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kDmaThreads), lds, s, g);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "conv_dma_kernel launch");
-}
-
-template <int BM, int BN, int WGM>
-int launch_conv(const ConvGeom& g0, hipStream_t s) {
-    static std::once_flag once;
-    auto k = conv_kernel<BM, BN, WGM>;
-    std::call_once(once, [&] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    });
-    ConvGeom g = g0;
-    g.tiles_n = g.Cout / BN;
-    const long long tiles = (long long)((g.M + BM - 1) / BM) * g.tiles_n;
-    if (tiles >= (1ll << 31)) return fail(MCGMIL_E_UNSUPPORTED, "too many tiles");
-    g.tiles = (int)tiles;
-    const size_t lds = (size_t)2 * (BM + BN) * kRowBytes;
-    hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(kConvThreads), lds, s, g);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "conv_kernel launch");
+    if (STATS) write_stats<4 * FI, WGM, BN>(st, wn * WN, wm, reinterpret_cast<float*>(smem), g.stats, gm,
+                                             g.Cout, tn * BN);
 }
 
 // ---- 3x3 / stride 1 / pad 1, 64 -> 64 channels (ResNet layer 1): halo-tile kernel.
-// The generic kernels fetch every input pixel once per tap (9x), which makes these layers L2-
-// bandwidth-bound (~520 TFLOP/s). Here a persistent workgroup (8 waves, one per CU) keeps the
-// whole 64 x 576 weight matrix in registers (each wave its 32 channels: 36 fragments) and, per
-// 256-pixel tile, DMAs the tile's input rows ONCE into LDS as a zero-padded patch: padded rows
-// P = n (H + 2) + ih + 1 of W + 2 pixels x 128 B (XOR-swizzled by patch pixel). All 9 taps then
-// read their A fragments from the patch at a tap offset -- no barrier inside a tile, 5x less L2
+// The whole 64 x 576 weight matrix lives in registers (each wave its 32 channels: 36 fragments).
+// Per 256-pixel tile the input rows are DMA'd ONCE into LDS as a zero-padded patch: padded rows
+// P = n (H + 2) + ih + 1 of W + 2 pixels x 128 B (XOR-swizzled by patch pixel). All 9 taps read
+// their A fragments from the patch at a tap offset -- no barrier inside a tile, 5x less L2
 // traffic per FLOP. The next tile's patch loads into the other buffer during this tile.
-constexpr int kHaloBM = 256;
-
 __device__ __forceinline__ uint32_t swz_lin(int p, int c) {     // swz() for a patch pixel index
     return (uint32_t)p * kRowBytes + (uint32_t)((c ^ ((p >> 1) & 7)) << 4);
 }
@@ -429,18 +370,20 @@ struct HaloGeom {
     ConvGeom g;
     int WP;         // W + 2 (padded row width)
     int NR;         // padded rows per patch (max over tiles)
-    int patch_px;   // NR * WP
+    int patch_px;   // NR * WP rounded up to whole 8-pixel DMA pieces
+    int tiles;
 };
 
-__global__ __launch_bounds__(kDmaThreads, 1) void conv3x3c64_kernel(const HaloGeom hg) {
+__global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom hg) {
+    constexpr bool STATS = false;   // measured: the statistics epilogue costs this kernel more than the
+                                    // separate statistics pass it saves (registers: 256 + spills)
     const ConvGeom& g = hg.g;
     constexpr int FI = 2, FJ = 4, KSTEPS = 18;          // wave: 64 pixels x 32 channels
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    const int t0 = (int)((long long)blockIdx.x * g.tiles / gridDim.x);
-    const int t1 = (int)((long long)(blockIdx.x + 1) * g.tiles / gridDim.x);
-    if (t0 >= t1) return;
+    const int t0 = (int)((long long)blockIdx.x * hg.tiles / gridDim.x);
+    const int t1 = (int)((long long)(blockIdx.x + 1) * hg.tiles / gridDim.x);
     const __amdgpu_buffer_rsrc_t xr = make_rsrc(g.x, g.x_bytes);
     const int HP = g.H + 2, WP = hg.WP;
     const size_t patch_bytes = (size_t)hg.patch_px * kRowBytes;
@@ -448,30 +391,35 @@ __global__ __launch_bounds__(kDmaThreads, 1) void conv3x3c64_kernel(const HaloGe
     // weights -> registers: K step s = (tap, half) covers k = 32 s .. 32 s + 31
     bf16x8 wf[KSTEPS][FI];
 #pragma unroll
-    for (int st = 0; st < KSTEPS; ++st)
+    for (int s = 0; s < KSTEPS; ++s)
 #pragma unroll
         for (int i = 0; i < FI; ++i) {
             const int co = wn * 32 + i * 16 + (lane & 15);
-            wf[st][i] = *reinterpret_cast<const bf16x8*>(g.w + (size_t)co * 576 + st * 32 + (lane >> 4) * 8);
+            wf[s][i] = *reinterpret_cast<const bf16x8*>(g.w + (size_t)co * 576 + s * 32 + (lane >> 4) * 8);
         }
+    LaneStats<4 * FI> st;
+    if (STATS) {
+        st.n = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4 * FI; ++c) st.x0[c] = st.S[c] = st.SS[c] = 0.f;
+    }
 
     // No per-tile integer division on the vector side: a tile's first pixel (n0, oh0, ow0) is
-    // scalar math, every lane-dependent offset below is split into (rows, cols) once per kernel and
-    // carried forward per tile / per DMA piece.
+    // scalar math, every lane-dependent offset below is split into (rows, cols) once per kernel
+    // and carried forward per tile / per DMA piece.
     const int OHW = g.OH * g.OW;
-    int dq[FJ], dr[FJ];                  // this lane's output pixel offset in the tile, per fragment
+    int dqr[FJ];      // this lane's output pixel offset in the tile per fragment: rows << 16 | cols
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
-        const int d = wm * 64 + j * 16 + (lane & 15);
-        dq[j] = d / g.OW;
-        dr[j] = d - dq[j] * g.OW;
+        const int d = wm * 64 + j * 16 + (lane & 15), q = d / g.OW;
+        dqr[j] = (q << 16) | (d - q * g.OW);
     }
     const int p0 = wave * 8 + (lane >> 3);       // first patch pixel this lane DMAs
     const int rr0 = p0 / WP, col0 = p0 - rr0 * WP;
     const int qstep = 64 / WP, rstep = 64 - qstep * WP;  // pieces advance by 64 patch pixels
 
     auto issue = [&](int tile, int buf) {
-        const int m0 = tile * kHaloBM;
+        const int m0 = tile * kBM;
         int n = m0 / OHW;
         int prel = (m0 - n * OHW) / g.OW + rr0;         // padded row (relative to image n) of p
         int col = col0;
@@ -479,15 +427,14 @@ __global__ __launch_bounds__(kDmaThreads, 1) void conv3x3c64_kernel(const HaloGe
             prel -= HP;
             ++n;
         }
-        unsigned char* L = smem + buf * patch_bytes;
+        unsigned char* Lp = smem + buf * patch_bytes;
         for (int piece = wave; piece * 8 < hg.patch_px; piece += 8) {
             const int p = piece * 8 + (lane >> 3);
             const int c = (lane & 7) ^ ((p >> 1) & 7);     // source chunk of this lane's slot
             const int ih = prel - 1, iw = col - 1;
-            const bool ok = p < hg.patch_px && n < g.N && (unsigned)ih < (unsigned)g.H &&
-                            (unsigned)iw < (unsigned)g.W;
+            const bool ok = n < g.N && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
             const uint32_t off = ((uint32_t)((n * g.H + ih) * g.W + iw) * 64u + (uint32_t)c * 8u) * 2u;
-            dma16(xr, L + piece * 1024, ok ? off : 0x80000000u, 0);
+            dma16(xr, Lp + piece * 1024, ok ? off : 0x80000000u, 0);
             col += rstep;
             prel += qstep;
             if (col >= WP) {
@@ -501,7 +448,7 @@ __global__ __launch_bounds__(kDmaThreads, 1) void conv3x3c64_kernel(const HaloGe
         }
     };
 
-    issue(t0, 0);
+    if (t0 < t1) issue(t0, 0);
     int buf = 0;
     for (int t = t0; t < t1; ++t) {
         // patch t landed; only the previous tile's epilogue stores (FI * FJ per lane) may still fly
@@ -509,13 +456,13 @@ __global__ __launch_bounds__(kDmaThreads, 1) void conv3x3c64_kernel(const HaloGe
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (t + 1 < t1) issue(t + 1, buf ^ 1);
-        const unsigned char* L = smem + buf * patch_bytes;
-        const int m0 = t * kHaloBM;
+        const unsigned char* Lp = smem + buf * patch_bytes;
+        const int m0 = t * kBM;
         const int n0 = m0 / OHW, r0m = m0 - n0 * OHW, oh0 = r0m / g.OW, ow0 = r0m - oh0 * g.OW;
         int pp[FJ];                                   // patch pixel of tap (0, 0) per fragment
 #pragma unroll
         for (int j = 0; j < FJ; ++j) {
-            int ow = ow0 + dr[j], oh = oh0 + dq[j], dn = 0;
+            int ow = ow0 + (dqr[j] & 0xFFFF), oh = oh0 + (dqr[j] >> 16), dn = 0;
             if (ow >= g.OW) {
                 ow -= g.OW;
                 ++oh;
@@ -528,11 +475,11 @@ __global__ __launch_bounds__(kDmaThreads, 1) void conv3x3c64_kernel(const HaloGe
             pp[j] = (dn * HP + oh - oh0) * WP + ow;
             if (pp[j] + 2 * WP + 2 >= hg.patch_px) pp[j] = 0;
         }
-        f32x4 acc[FI][FJ];
+        f32x4 acc[FJ][FI];
 #pragma unroll
-        for (int i = 0; i < FI; ++i)
+        for (int j = 0; j < FJ; ++j)
 #pragma unroll
-            for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int i = 0; i < FI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
             const int toff = (tap / 3) * WP + (tap % 3);
@@ -541,56 +488,127 @@ __global__ __launch_bounds__(kDmaThreads, 1) void conv3x3c64_kernel(const HaloGe
                 const int kq = ks * 4 + (lane >> 4);
                 bf16x8 xf[FJ];
 #pragma unroll
-                for (int j = 0; j < FJ; ++j) xf[j] = *reinterpret_cast<const bf16x8*>(L + swz_lin(pp[j] + toff, kq));
+                for (int j = 0; j < FJ; ++j) xf[j] = *reinterpret_cast<const bf16x8*>(Lp + swz_lin(pp[j] + toff, kq));
 #pragma unroll
                 for (int i = 0; i < FI; ++i)
 #pragma unroll
                     for (int j = 0; j < FJ; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tap * 2 + ks][i], xf[j], acc[i][j], 0, 0, 0);
+                        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tap * 2 + ks][i], xf[j], acc[j][i], 0, 0, 0);
             }
         }
+        const bool full = m0 + kBM <= g.M, first = t == t0;
 #pragma unroll
         for (int j = 0; j < FJ; ++j) {
             const int m = m0 + wm * 64 + j * 16 + (lane & 15);
-            if (m >= g.M) continue;
-            __bf16* dst = g.y + (size_t)m * 64 + wn * 32 + 4 * (lane >> 4);
-#pragma unroll
-            for (int i = 0; i < FI; ++i) {
-                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-                bf16x4 o;
-#pragma unroll
-                for (int v = 0; v < 4; ++v) o[v] = (__bf16)acc[i][j][v];
-                *reinterpret_cast<bf16x4*>(dst + i * 16) = o;
-            }
+            __bf16* dst = g.y + (size_t)(m < g.M ? m : 0) * 64 + wn * 32 + 4 * (lane >> 4);
+            if (full) store_fragment<FI, STATS, false>(acc[j], dst, true, first && j == 0, st);
+            else store_fragment<FI, STATS, true>(acc[j], dst, m < g.M, first && j == 0, st);
         }
         buf ^= 1;
     }
+    (void)st;
 }
 
-// launches the halo kernel when the layer and the LDS budget allow; returns 1 when it does not
-int launch_conv3x3c64(const ConvGeom& g0, hipStream_t s) {
-    if (g0.Cin != 64 || g0.Cout != 64 || g0.KH != 3 || g0.KW != 3 || g0.stride != 1 || g0.pad != 1) return 1;
+// ---- launch plan: which kernel, its grid and the statistics rows (Gm x 3 x Cout floats)
+struct Plan {
+    int kind = 0;          // 1: halo, 2: dma BN=128, 3: dma BN=64
+    int grid = 0;
+    int parts = 0;         // statistics rows
+    size_t lds = 0;
     HaloGeom hg;
-    hg.g = g0;
-    hg.WP = g0.W + 2;
-    // output rows a 256-pixel tile can span, + 2 halo rows, + 2 pad rows per image boundary crossed
-    const int rows = (kHaloBM - 1 + g0.OW - 1) / g0.OW + 1;
-    const int imgs = (kHaloBM - 1 + g0.OH * g0.OW - 1) / (g0.OH * g0.OW) + 1;
-    hg.NR = rows + 2 + 2 * (imgs - 1);
-    hg.patch_px = (hg.NR * hg.WP + 7) / 8 * 8;      // whole 8-pixel DMA pieces
-    const size_t lds = (size_t)2 * hg.patch_px * kRowBytes;
-    if (lds > 160 * 1024) return 1;
+};
+
+ConvGeom geom_of(const mcgmil_conv_args* a) {
+    ConvGeom g{};
+    g.x = static_cast<const __bf16*>(a->x);
+    g.w = static_cast<const __bf16*>(a->w);
+    g.y = static_cast<__bf16*>(a->y);
+    g.stats = a->stats;
+    g.N = a->batch; g.H = a->height; g.W = a->width; g.Cin = a->in_channels;
+    g.Cout = a->out_channels; g.KH = a->kernel_h; g.KW = a->kernel_w;
+    g.stride = a->stride; g.pad = a->pad;
+    g.OH = (g.H + 2 * g.pad - g.KH) / g.stride + 1;
+    g.OW = (g.W + 2 * g.pad - g.KW) / g.stride + 1;
+    g.M = g.N * g.OH * g.OW;
+    g.cin_tiles = g.Cin / 64;
+    g.KT = g.KH * g.KW * g.cin_tiles;
+    g.tiles_m = (g.M + kBM - 1) / kBM;
+    g.x_bytes = (uint32_t)((long long)g.N * g.H * g.W * g.Cin * 2);
+    g.w_bytes = (uint32_t)((long long)g.Cout * g.KH * g.KW * g.Cin * 2);
+    return g;
+}
+
+// MCGMIL_CONV_TILE=nohalo keeps layer-1 shapes on the generic kernel (A/B timing)
+Plan make_plan(ConvGeom& g) {
+    Plan p;
+    const int cus = cu_count();
+    const char* force = getenv("MCGMIL_CONV_TILE");
+    const bool halo_ok = !(force && !strcmp(force, "nohalo"));
+    if (halo_ok && g.Cin == 64 && g.Cout == 64 && g.KH == 3 && g.KW == 3 && g.stride == 1 && g.pad == 1) {
+        HaloGeom hg;
+        hg.WP = g.W + 2;
+        // output rows a tile can span, + 2 halo rows, + 2 pad rows per image boundary crossed
+        const int rows = (kBM - 1 + g.OW - 1) / g.OW + 1;
+        const int imgs = (kBM - 1 + g.OH * g.OW - 1) / (g.OH * g.OW) + 1;
+        hg.NR = rows + 2 + 2 * (imgs - 1);
+        hg.patch_px = (hg.NR * hg.WP + 7) / 8 * 8;
+        const size_t lds = (size_t)2 * hg.patch_px * kRowBytes;
+        if (lds <= 160 * 1024) {
+            hg.tiles = g.tiles_m;
+            g.tiles_n = 1;
+            g.Gm = hg.tiles < cus ? hg.tiles : cus;
+            hg.g = g;
+            p.kind = 1;
+            p.grid = g.Gm;
+            p.parts = 0;            // no statistics from this kernel (see conv3x3c64_kernel)
+            p.lds = lds;
+            p.hg = hg;
+            return p;
+        }
+    }
+    const int BN = g.Cout % 128 == 0 ? 128 : 64;
+    g.tiles_n = g.Cout / BN;
+    int gm = cus / g.tiles_n;
+    if (gm < 1) gm = 1;
+    if (gm > g.tiles_m) gm = g.tiles_m;
+    g.Gm = gm;
+    p.kind = BN == 128 ? 2 : 3;
+    p.grid = g.tiles_n * gm;
+    p.parts = gm;
+    p.lds = (size_t)kStages * (kBM + BN) * kRowBytes;
+    return p;
+}
+
+template <typename K>
+void raise_lds(K k) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+}
+
+int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
     static std::once_flag once;
     std::call_once(once, [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3c64_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        raise_lds(conv_dma_kernel<128, false>);
+        raise_lds(conv_dma_kernel<128, true>);
+        raise_lds(conv_dma_kernel<64, false>);
+        raise_lds(conv_dma_kernel<64, true>);
+        raise_lds(conv3x3c64_kernel);
     });
-    const long long tiles = ((long long)g0.M + kHaloBM - 1) / kHaloBM;
-    hg.g.tiles = (int)tiles;
-    const int grid = (int)(tiles < cu_count() ? tiles : cu_count());
-    hipLaunchKernelGGL(conv3x3c64_kernel, dim3((unsigned)grid), dim3(kDmaThreads), lds, s, hg);
+    const bool stats = g.stats != nullptr;
+    const dim3 grid((unsigned)p.grid), block(kThreads);
+    if (p.kind == 1) {
+        HaloGeom hg = p.hg;
+        hg.g = g;
+        hipLaunchKernelGGL(conv3x3c64_kernel, grid, block, p.lds, s, hg);
+    } else if (p.kind == 2) {
+        if (stats) hipLaunchKernelGGL((conv_dma_kernel<128, true>), grid, block, p.lds, s, g);
+        else hipLaunchKernelGGL((conv_dma_kernel<128, false>), grid, block, p.lds, s, g);
+    } else {
+        if (stats) hipLaunchKernelGGL((conv_dma_kernel<64, true>), grid, block, p.lds, s, g);
+        else hipLaunchKernelGGL((conv_dma_kernel<64, false>), grid, block, p.lds, s, g);
+    }
     hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "conv3x3c64_kernel launch");
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "convolution kernel launch");
 }
 
 // weights [Cout, Cin, KH, KW] (fp32 or bf16) -> [Cout, KH, KW, Cin] bf16
@@ -622,12 +640,10 @@ int validate(const mcgmil_conv_args* a) {
     const long long ow = ((long long)a->width + 2 * a->pad - a->kernel_w) / a->stride + 1;
     if (oh < 1 || ow < 1) return fail(MCGMIL_E_INVALID, "the kernel does not fit the padded input");
     const long long x_bytes = (long long)a->batch * a->height * a->width * a->in_channels * 2;
-    const long long y_elems = (long long)a->batch * oh * ow * a->out_channels;
     if (x_bytes >= (1ll << 31) || (long long)a->batch * oh * ow >= (1ll << 31) - kBM)
         return fail(MCGMIL_E_UNSUPPORTED, "input larger than 2 GiB or too many output pixels");
     if ((long long)a->out_channels * a->kernel_h * a->kernel_w * a->in_channels * 2 >= (1ll << 31))
         return fail(MCGMIL_E_UNSUPPORTED, "weights larger than 2 GiB");
-    (void)y_elems;
     return MCGMIL_OK;
 }
 
@@ -659,42 +675,25 @@ int mcgmil_pack_conv_weights(const mcgmil_conv_args* a, const void* weight, int3
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "pack_conv_weights_kernel launch");
 }
 
+int mcgmil_conv_stats_parts(const mcgmil_conv_args* a, int32_t* parts) {
+    int rc = validate(a);
+    if (rc) return rc;
+    if (!parts) return fail(MCGMIL_E_INVALID, "parts is NULL");
+    ConvGeom g = geom_of(a);
+    *parts = make_plan(g).parts;
+    return MCGMIL_OK;
+}
+
 int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream) {
     int rc = validate(a);
     if (rc) return rc;
     if (!a->x || !a->w || !a->y) return fail(MCGMIL_E_INVALID, "NULL x, w or y");
     if (((uintptr_t)a->x | (uintptr_t)a->w | (uintptr_t)a->y) & 15u)
         return fail(MCGMIL_E_ALIGN, "x, w and y must be 16-byte aligned");
-    ConvGeom g;
-    g.x = static_cast<const __bf16*>(a->x);
-    g.w = static_cast<const __bf16*>(a->w);
-    g.y = static_cast<__bf16*>(a->y);
-    g.N = a->batch; g.H = a->height; g.W = a->width; g.Cin = a->in_channels;
-    g.Cout = a->out_channels; g.KH = a->kernel_h; g.KW = a->kernel_w;
-    g.stride = a->stride; g.pad = a->pad;
-    g.OH = (g.H + 2 * g.pad - g.KH) / g.stride + 1;
-    g.OW = (g.W + 2 * g.pad - g.KW) / g.stride + 1;
-    g.M = g.N * g.OH * g.OW;
-    g.cin_tiles = g.Cin / 64;
-    g.KT = g.KH * g.KW * g.cin_tiles;
-    g.x_bytes = (uint32_t)((long long)g.N * g.H * g.W * g.Cin * 2);
-    g.w_bytes = (uint32_t)((long long)g.Cout * g.KH * g.KW * g.Cin * 2);
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    // tile shape: 128 x 128 when Cout allows, else 256 x 64 (the same 64 x 64 block per wave);
-    // MCGMIL_CONV_TILE=128x64|256x64|128x128|dma256x64|dma512x64|dma256x128x2 forces one (A/B)
-    const char* force = getenv("MCGMIL_CONV_TILE");
-    if (force && !strcmp(force, "128x64")) return launch_conv<128, 64, 2>(g, s);
-    if (force && !strcmp(force, "256x64")) return launch_conv<256, 64, 4>(g, s);
-    if (force && !strcmp(force, "128x128") && g.Cout % 128 == 0) return launch_conv<128, 128, 2>(g, s);
-    if (force && !strcmp(force, "dma256x64")) return launch_conv_dma<256, 64, 4, 3>(g, s);
-    if (!(force && !strcmp(force, "nohalo"))) {
-        const int rc = launch_conv3x3c64(g, s);
-        if (rc != 1) return rc;
-    }
-    if (force && !strcmp(force, "dma512x64")) return launch_conv_dma<512, 64, 8, 2>(g, s);
-    if (force && !strcmp(force, "dma256x128x2") && g.Cout % 128 == 0) return launch_conv_dma<256, 128, 4, 2>(g, s);
-    if (g.Cout % 128 == 0) return launch_conv_dma<256, 128, 4, 3>(g, s);
-    return launch_conv_dma<256, 64, 4, 3>(g, s);
+    if ((uintptr_t)a->stats & 3u) return fail(MCGMIL_E_ALIGN, "stats must be 4-byte aligned");
+    ConvGeom g = geom_of(a);
+    const Plan p = make_plan(g);
+    return launch(g, p, reinterpret_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

@@ -28,7 +28,7 @@ EXPORTED = (
     "mcgmil_image_to_bag", "mcgmil_attention_maps", "mcgmil_reconstruct_image",
     # include/mcgmil_features.h
     "mcgmil_bn_args_size", "mcgmil_bn_workspace_size", "mcgmil_batchnorm_act",
-    "mcgmil_conv_args_size", "mcgmil_pack_conv_weights", "mcgmil_conv2d",
+    "mcgmil_conv_args_size", "mcgmil_pack_conv_weights", "mcgmil_conv_stats_parts", "mcgmil_conv2d",
     "mcgmil_stem_args_size", "mcgmil_stem_packed_size", "mcgmil_pack_stem_weights",
     "mcgmil_stem_workspace_size", "mcgmil_stem_forward",
 )
@@ -81,7 +81,7 @@ class ConvArgs(ctypes.Structure):
         ("in_channels", ctypes.c_int32), ("out_channels", ctypes.c_int32),
         ("kernel_h", ctypes.c_int32), ("kernel_w", ctypes.c_int32), ("stride", ctypes.c_int32),
         ("pad", ctypes.c_int32), ("reserved", ctypes.c_int32),
-        ("x", _vp), ("w", _vp), ("y", _vp),
+        ("x", _vp), ("w", _vp), ("y", _vp), ("stats", _vp),
     ]
 
 
@@ -107,9 +107,9 @@ class BnArgs(ctypes.Structure):
         ("running_mean", _vp), ("running_var", _vp), ("eps", ctypes.c_double),
         ("relu", ctypes.c_int32), ("batch", ctypes.c_int32), ("height", ctypes.c_int32),
         ("width", ctypes.c_int32), ("pool_kernel", ctypes.c_int32), ("pool_stride", ctypes.c_int32),
-        ("pool_pad", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("pool_pad", ctypes.c_int32), ("num_partials", ctypes.c_int32),
         ("batch_mean", _vp), ("batch_invstd", _vp),
-        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t), ("partials", _vp),
     ]
 
 
@@ -173,6 +173,8 @@ def load():
     L.mcgmil_conv_args_size.restype = ctypes.c_size_t
     L.mcgmil_pack_conv_weights.argtypes = [pc, _vp, ctypes.c_int32, _vp, _vp]
     L.mcgmil_pack_conv_weights.restype = ctypes.c_int
+    L.mcgmil_conv_stats_parts.argtypes = [pc, ctypes.POINTER(ctypes.c_int32)]
+    L.mcgmil_conv_stats_parts.restype = ctypes.c_int
     L.mcgmil_conv2d.argtypes = [pc, _vp]
     L.mcgmil_conv2d.restype = ctypes.c_int
     ps = ctypes.POINTER(StemArgs)

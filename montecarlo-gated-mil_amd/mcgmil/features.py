@@ -124,9 +124,11 @@ def packed_conv_weight(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     return packed
 
 
-def conv2d(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+def conv2d(conv: nn.Conv2d, x: torch.Tensor, stats: bool = False):
     """conv(x) for a channels-last bf16 activation (see conv_fusable) on the MFMA kernel; returns a
-    channels-last bf16 tensor."""
+    channels-last bf16 tensor, or with stats=True (y, partials): the BatchNorm statistics of y
+    as [parts, 3, Cout] (count, mean, M2) blocks for batchnorm_act(..., partials=...), or None
+    where the layer's kernel emits none (the 3x3 64 -> 64 halo kernel)."""
     if not conv_fusable(conv, x):
         raise ValueError("conv2d needs a CUDA channels-last bf16 activation, a bias-free groups=1 "
                          "convolution with 64k channels and no autograd (see conv_fusable)")
@@ -138,9 +140,16 @@ def conv2d(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
                     memory_format=torch.channels_last)
     w = packed_conv_weight(conv, x)
     a.x, a.w, a.y = (ctypes.c_void_p(t.data_ptr()) for t in (x, w, y))
+    part = None
+    if stats:
+        n = ctypes.c_int32()
+        _lib.check(L.mcgmil_conv_stats_parts(ctypes.byref(a), ctypes.byref(n)), "mcgmil_conv_stats_parts")
+        if n.value > 0:          # 0: this layer's kernel emits no statistics
+            part = torch.empty((n.value, 3, a.out_channels), dtype=torch.float32, device=x.device)
+            a.stats = ctypes.c_void_p(part.data_ptr())
     stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
     _lib.check(L.mcgmil_conv2d(ctypes.byref(a), stream), "mcgmil_conv2d")
-    return y
+    return (y, part) if stats else y
 
 
 def run_conv(layer: nn.Module, x: torch.Tensor) -> torch.Tensor:
@@ -173,10 +182,12 @@ def _pool_params(pool) -> Optional[tuple]:
 
 def batchnorm_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool,
                   residual: Optional[torch.Tensor] = None,
-                  pool: Optional[nn.MaxPool2d] = None) -> torch.Tensor:
+                  pool: Optional[nn.MaxPool2d] = None,
+                  partials: Optional[torch.Tensor] = None) -> torch.Tensor:
     """relu?(bn(x) [+ residual]) for a channels-last [N, C, H, W] activation (see fusable), or
     pool(relu?(bn(x))) with a fusable max-pool (the ResNet stem) without materialising the
-    activation."""
+    activation. `partials` ([parts, 3, C] from conv2d(..., stats=True)) supplies the batch
+    statistics of x, so x is read once."""
     if not fusable(x, bn, residual):
         raise ValueError("batchnorm_act needs a CUDA channels-last bf16/fp32 activation with "
                          "C % 8 == 0, C <= 2048 and no autograd (see mcgmil.features.fusable)")
@@ -208,6 +219,11 @@ def batchnorm_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool,
     a.x, a.y, a.residual = p(x), p(y), p(residual)
     a.gamma, a.beta, a.running_mean, a.running_var = p(gamma), p(beta), p(rmean), p(rvar)
     a.eps, a.relu = float(bn.eps), int(bool(relu))
+    if partials is not None and use_batch:
+        if partials.dim() != 3 or partials.shape[1:] != (3, C) or not partials.is_contiguous() or \
+                partials.dtype != torch.float32 or partials.device != dev:
+            raise ValueError("partials must be a contiguous fp32 [parts, 3, C] tensor on x's device")
+        a.partials, a.num_partials = p(partials), partials.shape[0]
     n = ctypes.c_size_t()
     _lib.check(L.mcgmil_bn_workspace_size(ctypes.byref(a), ctypes.byref(n)), "mcgmil_bn_workspace_size")
     ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
@@ -348,3 +364,19 @@ def run_stem(conv: nn.Module, bn: nn.Module, pool: Optional[nn.Module], x: torch
     if x.is_cuda and x.dim() == 4:
         x = x.contiguous(memory_format=torch.channels_last)
     return bn_act(bn, conv(x), True, pool=pool)
+
+
+def conv_bn_act(conv: nn.Module, bn: nn.Module, x: torch.Tensor, relu: bool,
+                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The blocks' `relu?(bn(conv(x)) [+ residual])`: on the GPU the MFMA convolution also emits
+    the BatchNorm batch statistics of its output (when the BN normalises with them), and the fused
+    BN consumes them -- the activation is written once and read once. Else run_conv + bn_act."""
+    if isinstance(conv, nn.Conv2d) and isinstance(bn, nn.BatchNorm2d) and conv_fusable(conv, x):
+        use_batch = bn.training or bn.running_mean is None or bn.running_var is None
+        if use_batch:
+            y, part = conv2d(conv, x, stats=True)
+            if fusable(y, bn, residual):
+                return batchnorm_act(y, bn, relu, residual, partials=part)
+            return bn_act(bn, y, relu, residual)
+        return bn_act(bn, conv2d(conv, x), relu, residual)
+    return bn_act(bn, run_conv(conv, x), relu, residual)

@@ -12,9 +12,10 @@ with random initialisation and warns (load a checkpoint to get trained weights).
 
 The stem `maxpool(relu(bn1(conv1(x))))` goes through `features.run_stem` (one fused MFMA
 convolution + statistics + BN/ReLU/pool call on the GPU) and every
-`relu?(bn(conv(x)) [+ identity])` of the blocks goes through `features.run_conv` and
-`features.bn_act`: on the GPU with channels-last bf16 activations they are the MFMA
-implicit-GEMM convolution and one fused HIP BatchNorm(+add)(+ReLU) (include/mcgmil_features.h);
+`relu?(bn(conv(x)) [+ identity])` of the blocks goes through `features.conv_bn_act`: on the GPU
+with channels-last bf16 activations that is the MFMA implicit-GEMM convolution (which also emits
+the BN batch statistics of its output) and one fused HIP BatchNorm(+add)(+ReLU)
+(include/mcgmil_features.h);
 elsewhere (CPU, autograd, fp32) they are the torch layers.
 """
 import warnings
@@ -22,7 +23,7 @@ import warnings
 import torch
 import torch.nn as nn
 
-from .features import bn_act, run_conv, run_stem
+from .features import conv_bn_act, run_stem
 
 
 class Identity(nn.Module):
@@ -45,7 +46,7 @@ def _identity(down, x):
     if down is None:
         return x
     if isinstance(down, nn.Sequential) and len(down) == 2 and isinstance(down[1], nn.BatchNorm2d):
-        return bn_act(down[1], run_conv(down[0], x), False)
+        return conv_bn_act(down[0], down[1], x, False)
     return down(x)
 
 
@@ -67,8 +68,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         idt = _identity(self.downsample, x)
-        y = bn_act(self.bn1, run_conv(self.conv1, x), True)
-        return bn_act(self.bn2, run_conv(self.conv2, y), True, idt)
+        y = conv_bn_act(self.conv1, self.bn1, x, True)
+        return conv_bn_act(self.conv2, self.bn2, y, True, idt)
 
 
 class Bottleneck(nn.Module):
@@ -87,9 +88,9 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         idt = _identity(self.downsample, x)
-        y = bn_act(self.bn1, run_conv(self.conv1, x), True)
-        y = bn_act(self.bn2, run_conv(self.conv2, y), True)
-        return bn_act(self.bn3, run_conv(self.conv3, y), True, idt)
+        y = conv_bn_act(self.conv1, self.bn1, x, True)
+        y = conv_bn_act(self.conv2, self.bn2, y, True)
+        return conv_bn_act(self.conv3, self.bn3, y, True, idt)
 
 
 class ResNet(nn.Module):

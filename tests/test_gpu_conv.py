@@ -102,3 +102,81 @@ def test_conv_fusable_gates(cuda):
         assert not conv_fusable(conv, x.float().contiguous(memory_format=torch.channels_last))
     with torch.autocast("cuda", dtype=torch.bfloat16):
         assert not conv_fusable(conv, x)                      # grad enabled, weight needs grad
+
+
+def _bn64(C, dev, seed):
+    from mcgmil.resnet import deactivate_batchnorm
+    g = torch.Generator().manual_seed(seed)
+    bn = nn.BatchNorm2d(C)
+    with torch.no_grad():
+        bn.weight.copy_(torch.randn(C, generator=g) * 0.5 + 1.0)
+        bn.weight[::5] *= -1.0
+        bn.bias.copy_(torch.randn(C, generator=g) * 0.3)
+    deactivate_batchnorm(bn)
+    return bn.to(dev).eval()
+
+
+# conv + batch-statistics BN (+ residual) + ReLU, the statistics taken from the convolution's
+# epilogue: every kernel (halo 3x3 64->64, 256 x 64 and 256 x 128 tiles), ragged pixel counts,
+# several channel tiles, and an input offset that makes mean >> std for the statistics
+STATS_SHAPES = [
+    (3, 64, 56, 56, 64, 3, 1, 1, 0.0),
+    (9, 64, 8, 6, 64, 3, 1, 1, 0.0),
+    (2, 64, 28, 28, 128, 3, 2, 1, 0.0),
+    (3, 128, 13, 11, 256, 3, 1, 1, 0.0),
+    (2, 256, 7, 7, 512, 1, 2, 0, 0.0),
+    (5, 64, 9, 11, 192, 3, 1, 1, 0.0),
+    (3, 64, 20, 20, 64, 3, 1, 1, 4.0),
+    (2, 128, 10, 10, 128, 3, 1, 1, 4.0),
+]
+
+
+@pytest.mark.parametrize("shape", STATS_SHAPES)
+@pytest.mark.parametrize("residual", [False, True])
+def test_conv_bn_act_fused_statistics(cuda, shape, residual):
+    """|y - ref| <= |a_c| (2^-8 |conv| + 1e-5 conv(|x|,|w|)) + 2^-8 |y| + 2e-3 |a_c| std_c: the
+    convolution's rounding, the fused BN's rounding, and the statistics of rounded values."""
+    from mcgmil.features import conv2d, conv_bn_act
+    N, Cin, H, W, Cout, k, s, p, off = shape
+    conv = _layer(Cin, Cout, k, s, p, cuda, Cin * 3 + Cout + k)
+    bn = _bn64(Cout, cuda, Cout + k)
+    g = torch.Generator(device=cuda).manual_seed(N * H + W + Cout)
+    x = (torch.randn(N, Cin, H, W, device=cuda, generator=g).relu_() + off).bfloat16()
+    x = x.contiguous(memory_format=torch.channels_last)
+    oh, ow = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    idt = torch.randn(N, Cout, oh, ow, device=cuda, generator=g).bfloat16().contiguous(
+        memory_format=torch.channels_last) if residual else None
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv_bn_act(conv, bn, x, True, idt)
+        _, part = conv2d(conv, x, stats=True)
+    if part is not None:
+        assert part.shape[1:] == (3, Cout)
+        assert float(part[:, 0, :].sum(0).min()) == N * oh * ow == float(part[:, 0, :].sum(0).max())
+    else:
+        assert (Cin, Cout, k, s, p) == (64, 64, 3, 1, 1)        # the halo kernel
+    wb = conv.weight.detach().bfloat16().double()
+    with torch.no_grad():
+        c = F.conv2d(x.double(), wb, None, s, p)
+        mag = F.conv2d(x.double().abs(), wb.abs(), None, s, p)
+    mean, var = c.mean(dim=(0, 2, 3)), c.var(dim=(0, 2, 3), unbiased=False)
+    a = bn.weight.double() / torch.sqrt(var + bn.eps)
+    b = bn.bias.double() - mean * a
+    ref = c * a[None, :, None, None] + b[None, :, None, None]
+    if residual:
+        ref = ref + idt.double()
+    bound = a.abs()[None, :, None, None] * (2.0 ** -8 * c.abs() + 1e-5 * mag) + 2.0 ** -8 * ref.abs() + \
+        (2e-3 * a.abs() * torch.sqrt(var))[None, :, None, None] + 1e-6
+    ref = torch.relu(ref)
+    err = (y.double() - ref).abs()
+    assert torch.all(err <= bound), float((err - bound).max())
+
+
+def test_conv_statistics_deterministic(cuda):
+    from mcgmil.features import conv2d
+    conv = _layer(128, 256, 3, 1, 1, cuda, 7)
+    x = torch.randn(6, 128, 28, 28, device=cuda).relu_().bfloat16().contiguous(memory_format=torch.channels_last)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y1, p1 = conv2d(conv, x, stats=True)
+        y2, p2 = conv2d(conv, x, stats=True)
+        y3 = conv2d(conv, x)
+    assert torch.equal(y1, y2) and torch.equal(p1, p2) and torch.equal(y1, y3)
