@@ -509,9 +509,205 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
     (void)st;
 }
 
+// ---- 3x3 / stride 1 / pad 1 with Cin = 64 k >= 128 and Cout % 128 == 0 (ResNet layers 2-4):
+// halo tiles with streamed weights. conv_dma_kernel re-fetches each pixel once per tap (48 KB of
+// L2 traffic per 256 x 128 x 64 step); here a (pixel tile, 64-channel chunk cc) patch is DMA'd
+// once into LDS and read by all 9 taps, and only the 16-KB weight tile of each (tap, cc) step is
+// streamed (~23 KB per step). Steps run tile-major, then cc, then tap; one barrier per step:
+//  - weights of step s + 1 go into the other of two 16-KB stages right after the barrier of s;
+//  - the patch of the NEXT (tile, cc) is loaded one 1-KiB piece per wave per tap (taps 0..7),
+//    issued after that step's weights, into the other of two 64-KB patch buffers (fixed 512
+//    pixels; pieces past the patch read out of range, i.e. zeros, without memory traffic);
+//  - so the wait at the top of step s is vmcnt(1) after a patch piece, vmcnt(FI * FJ) after a
+//    tile's epilogue stores, else vmcnt(0) (vmcnt retires in order).
+// Workgroups are mapped like conv_dma_kernel (one channel tile each, contiguous pixel tiles), so
+// the BatchNorm statistics epilogue is the same.
+constexpr int kPatchPx = 512;
+
+template <bool STATS>
+__global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeom hg) {
+    const ConvGeom& g = hg.g;
+    constexpr int BN = 128, WGM = 4, WGN = 2, WM = 64, WN = 64, FI = 4, FJ = 4;
+    constexpr size_t PATCH = (size_t)kPatchPx * kRowBytes, WSTAGE = (size_t)BN * kRowBytes;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave / WGN, wn = wave % WGN;
+    const int L = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int tn = L % g.tiles_n, gm = L / g.tiles_n;
+    const int tm0 = (int)((long long)gm * g.tiles_m / g.Gm);
+    const int tm1 = (int)((long long)(gm + 1) * g.tiles_m / g.Gm);
+    const int CC = g.cin_tiles, SPT = 9 * CC;            // steps per tile
+    const int steps = (tm1 - tm0) * SPT;
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(g.x, g.x_bytes);
+    const __amdgpu_buffer_rsrc_t wr = make_rsrc(g.w, g.w_bytes);
+    const int HP = g.H + 2, WP = hg.WP, OHW = g.OH * g.OW;
+    unsigned char* patch0 = smem;                        // [2][kPatchPx][128 B]
+    unsigned char* wst0 = smem + 2 * PATCH;              // [2][BN][128 B]
+
+    // weights: 2 pieces per wave per step (rows 8 (wave + 8 j) + lane / 8 of the channel tile)
+    const uint32_t K = (uint32_t)(9 * g.Cin);
+    uint32_t wrow[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int r = 8 * (wave + 8 * j) + (lane >> 3);
+        wrow[j] = ((uint32_t)(tn * BN + r) * K + (uint32_t)(((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
+    }
+    auto issue_w = [&](int step, int buf) {     // step -> (tap, cc): K tile kt = tap * CC + cc
+        const int r = step % SPT, cc = r / 9, tap = r - cc * 9;
+        const uint32_t soff = (uint32_t)(tap * CC + cc) * (kBK * 2u);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) dma16(wr, wst0 + buf * WSTAGE + (wave + 8 * j) * 1024, wrow[j], soff);
+    };
+    // patch pieces: wave's piece k (k = 0..7) covers patch pixels 8 (wave + 8 k) .. + 7; the lane's
+    // pixel advances by 64 per piece, carried as (image, padded row, column) -- no divisions
+    const int p0 = wave * 8 + (lane >> 3);
+    const int rr0 = p0 / WP, col0 = p0 - rr0 * WP;
+    const int qstep = 64 / WP, rstep = 64 - qstep * WP;
+    int pn = 0, prel = 0, pcol = 0, pcc = 0;
+    unsigned char* pdst = patch0;
+    auto patch_begin = [&](int tm, int cc, int buf) {
+        const int m0 = tm * kBM;
+        pn = m0 / OHW;
+        prel = (m0 - pn * OHW) / g.OW + rr0;
+        pcol = col0;
+        while (prel >= HP) {
+            prel -= HP;
+            ++pn;
+        }
+        pcc = cc;
+        pdst = patch0 + buf * PATCH;
+    };
+    auto patch_piece = [&](int k) {
+        const int p = 8 * (wave + 8 * k) + (lane >> 3);
+        const int c = (lane & 7) ^ ((p >> 1) & 7);
+        const int ih = prel - 1, iw = pcol - 1;
+        const bool ok = p < hg.patch_px && pn < g.N && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        const uint32_t off = ((uint32_t)((pn * g.H + ih) * g.W + iw) * (uint32_t)g.Cin +
+                              (uint32_t)(pcc * 64 + c * 8)) * 2u;
+        dma16(xr, pdst + (wave + 8 * k) * 1024, ok ? off : 0x80000000u, 0);
+        pcol += rstep;
+        prel += qstep;
+        if (pcol >= WP) {
+            pcol -= WP;
+            ++prel;
+        }
+        while (prel >= HP) {
+            prel -= HP;
+            ++pn;
+        }
+    };
+
+    f32x4 acc[FJ][FI];
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)
+#pragma unroll
+        for (int i = 0; i < FI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    LaneStats<4 * FI> st;
+    if (STATS) {
+        st.n = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4 * FI; ++c) st.x0[c] = st.S[c] = st.SS[c] = 0.f;
+    }
+    int dqr[FJ];      // this lane's output pixel offset in the tile per fragment: rows << 16 | cols
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+        const int d = wm * WM + j * 16 + (lane & 15), q = d / g.OW;
+        dqr[j] = (q << 16) | (d - q * g.OW);
+    }
+    int pp[FJ];
+    auto tile_setup = [&](int tm) {
+        const int m0 = tm * kBM;
+        const int n0 = m0 / OHW, r0m = m0 - n0 * OHW, oh0 = r0m / g.OW, ow0 = r0m - oh0 * g.OW;
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+            int ow = ow0 + (dqr[j] & 0xFFFF), oh = oh0 + (dqr[j] >> 16), dn = 0;
+            if (ow >= g.OW) {
+                ow -= g.OW;
+                ++oh;
+            }
+            while (oh >= g.OH) {
+                oh -= g.OH;
+                ++dn;
+            }
+            pp[j] = (dn * HP + oh - oh0) * WP + ow;         // rows past M: a finite patch row
+            if (pp[j] + 2 * WP + 2 >= hg.patch_px) pp[j] = 0;
+        }
+    };
+
+    if (steps <= 0) return;
+    // prologue: the first (tile, cc) patch whole, the first weights
+    patch_begin(tm0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) patch_piece(k);
+    issue_w(0, 0);
+    tile_setup(tm0);
+    int tm = tm0, r = 0, pbuf = 0;     // r = step within the tile
+    int wait_kind = 0;                 // 0: vmcnt(0), 1: a patch piece after the weights, 2: stores
+    for (int s = 0; s < steps; ++s) {
+        if (wait_kind == 1) wait_vmcnt<1>();
+        else if (wait_kind == 2) wait_vmcnt<FI * FJ>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const int cc = r / 9, tap = r - cc * 9;
+        wait_kind = 0;
+        if (s + 1 < steps) issue_w(s + 1, (s + 1) & 1);
+        // the next (tile, cc) patch: begun at tap 0, one piece per tap 0..7
+        const bool more_patch = (r + 9 < SPT) || (tm + 1 < tm1);
+        if (more_patch && tap < 8) {
+            if (tap == 0) {
+                if (cc + 1 < CC) patch_begin(tm, cc + 1, pbuf ^ 1);
+                else patch_begin(tm + 1, 0, pbuf ^ 1);
+            }
+            patch_piece(tap);
+            wait_kind = 1;
+        }
+        // compute step s: A from the patch at the tap offset, B from the weight stage
+        {
+            const unsigned char* A = patch0 + pbuf * PATCH;
+            const unsigned char* B = wst0 + (s & 1) * WSTAGE;
+            const int toff = (tap / 3) * WP + (tap % 3);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int kq = ks * 4 + (lane >> 4);
+                bf16x8 wf[FI], xf[FJ];
+#pragma unroll
+                for (int i = 0; i < FI; ++i)
+                    wf[i] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WN + i * 16 + (lane & 15), kq));
+#pragma unroll
+                for (int j = 0; j < FJ; ++j) xf[j] = *reinterpret_cast<const bf16x8*>(A + swz_lin(pp[j] + toff, kq));
+#pragma unroll
+                for (int i = 0; i < FI; ++i)
+#pragma unroll
+                    for (int j = 0; j < FJ; ++j)
+                        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[j][i], 0, 0, 0);
+            }
+        }
+        if (tap == 8) pbuf ^= 1;                        // next cc (or tile) uses the other patch
+        if (++r == SPT) {
+            const bool full = (tm + 1) * kBM <= g.M, first = tm == tm0;
+#pragma unroll
+            for (int j = 0; j < FJ; ++j) {
+                const int m = tm * kBM + wm * WM + j * 16 + (lane & 15);
+                __bf16* dst = g.y + (size_t)(m < g.M ? m : 0) * g.Cout + tn * BN + wn * WN + 4 * (lane >> 4);
+                if (full) store_fragment<FI, STATS, false>(acc[j], dst, true, first && j == 0, st);
+                else store_fragment<FI, STATS, true>(acc[j], dst, m < g.M, first && j == 0, st);
+#pragma unroll
+                for (int i = 0; i < FI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            wait_kind = 2;
+            r = 0;
+            ++tm;
+            if (tm < tm1) tile_setup(tm);
+        }
+    }
+    if (STATS) write_stats<4 * FI, WGM, BN>(st, wn * WN, wm, reinterpret_cast<float*>(smem), g.stats, gm,
+                                             g.Cout, tn * BN);
+}
+
 // ---- launch plan: which kernel, its grid and the statistics rows (Gm x 3 x Cout floats)
 struct Plan {
-    int kind = 0;          // 1: halo, 2: dma BN=128, 3: dma BN=64
+    int kind = 0;          // 1: halo 64 -> 64, 2: dma BN=128, 3: dma BN=64, 4: halo, streamed weights
     int grid = 0;
     int parts = 0;         // statistics rows
     size_t lds = 0;
@@ -571,6 +767,30 @@ Plan make_plan(ConvGeom& g) {
     int gm = cus / g.tiles_n;
     if (gm < 1) gm = 1;
     if (gm > g.tiles_m) gm = g.tiles_m;
+    // measured (scripts/probe_conv.py, one process): +8% at 28 x 28 (layer 2), neutral at 14 x 14,
+    // -2% at 7 x 7, where a tile spans many images and the patch is mostly halo
+    if (halo_ok && g.Cin >= 128 && BN == 128 && g.KH == 3 && g.KW == 3 && g.stride == 1 && g.pad == 1 &&
+        g.OW >= 20) {
+        HaloGeom hg;
+        hg.WP = g.W + 2;
+        const int rows = (kBM - 1 + g.OW - 1) / g.OW + 1;
+        const int imgs = (kBM - 1 + g.OH * g.OW - 1) / (g.OH * g.OW) + 1;
+        hg.NR = rows + 2 + 2 * (imgs - 1);
+        hg.patch_px = hg.NR * hg.WP;
+        if (hg.patch_px <= kPatchPx) {
+            hg.tiles = g.tiles_m;
+            g.Gm = gm;
+            hg.g = g;
+            p.kind = 4;
+            p.grid = g.tiles_n * gm;
+            p.parts = gm;
+            p.lds = (size_t)2 * kPatchPx * kRowBytes + (size_t)2 * 128 * kRowBytes;
+            p.hg = hg;
+            return p;
+        }
+    }
+    if (gm < 1) gm = 1;
+    if (gm > g.tiles_m) gm = g.tiles_m;
     g.Gm = gm;
     p.kind = BN == 128 ? 2 : 3;
     p.grid = g.tiles_n * gm;
@@ -593,6 +813,8 @@ int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
         raise_lds(conv_dma_kernel<64, false>);
         raise_lds(conv_dma_kernel<64, true>);
         raise_lds(conv3x3c64_kernel);
+        raise_lds(conv3x3_halo_kernel<false>);
+        raise_lds(conv3x3_halo_kernel<true>);
     });
     const bool stats = g.stats != nullptr;
     const dim3 grid((unsigned)p.grid), block(kThreads);
@@ -600,6 +822,11 @@ int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
         HaloGeom hg = p.hg;
         hg.g = g;
         hipLaunchKernelGGL(conv3x3c64_kernel, grid, block, p.lds, s, hg);
+    } else if (p.kind == 4) {
+        HaloGeom hg = p.hg;
+        hg.g = g;
+        if (stats) hipLaunchKernelGGL(conv3x3_halo_kernel<true>, grid, block, p.lds, s, hg);
+        else hipLaunchKernelGGL(conv3x3_halo_kernel<false>, grid, block, p.lds, s, hg);
     } else if (p.kind == 2) {
         if (stats) hipLaunchKernelGGL((conv_dma_kernel<128, true>), grid, block, p.lds, s, g);
         else hipLaunchKernelGGL((conv_dma_kernel<128, false>), grid, block, p.lds, s, g);

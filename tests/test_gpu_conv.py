@@ -34,6 +34,11 @@ SHAPES = [
     (3, 64, 30, 17, 64, 3, 1, 1),
     (2, 64, 20, 62, 64, 3, 1, 1),
     (1, 64, 5, 70, 64, 3, 1, 1),
+    # 3x3 / stride 1 halo kernel with streamed weights (Cin >= 128): many small images per tile,
+    # 3 input-channel chunks, 2 channel tiles, and a row too wide for the patch (generic kernel)
+    (4, 128, 25, 20, 128, 3, 1, 1),
+    (2, 192, 17, 30, 256, 3, 1, 1),
+    (1, 128, 6, 80, 128, 3, 1, 1),
 ]
 
 
@@ -128,6 +133,8 @@ STATS_SHAPES = [
     (5, 64, 9, 11, 192, 3, 1, 1, 0.0),
     (3, 64, 20, 20, 64, 3, 1, 1, 4.0),
     (2, 128, 10, 10, 128, 3, 1, 1, 4.0),
+    (4, 128, 25, 20, 128, 3, 1, 1, 0.0),
+    (2, 192, 17, 30, 256, 3, 1, 1, 2.0),
 ]
 
 
