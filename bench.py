@@ -100,10 +100,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", 0 if args.same_device else local)
+    torch.cuda.set_device(dev)          # before the process group, so RCCL binds this rank's GPU
     if world > 1:
         dist.init_process_group(args.dist_backend)
-    dev = torch.device("cuda", 0 if args.same_device else local)
-    torch.cuda.set_device(dev)
 
     if args.workload == "cfg5":
         import bench_cfg5
