@@ -241,9 +241,7 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
     for (int t = t0; t < t1; ++t) {
         const int cur = (t - t0) & 1;
         const bool more = t + 1 < t1;
-#ifndef MCGMIL_STEM_LATE_STAGE   // A/B variant: stage the next tile after this one's compute
-        if (more) stage(t + 1, cur ^ 1);
-#endif
+        if (more) stage(t + 1, cur ^ 1);     // (staging after the compute measured no faster)
         const int n = t / g.TPI, oh = (t - n * g.TPI) * kTH + wave;
         if (oh < g.OH) {
             const uint32_t* L = lds + cur * buf_dw;
@@ -290,19 +288,12 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
                 for (int h = 0; h < 2; ++h) {
                     const int pp = (lane >> 3) + 8 * h, c = lane & 7;
                     const bf16x8 v = *reinterpret_cast<const bf16x8*>(scratch + pp * 64 + ((c ^ (pp & 7)) << 3));
-#ifndef MCGMIL_STEM_NOSTORE   // timing-only variant: no activation stores
                     if (16 * f + pp < g.OW)
                         *reinterpret_cast<bf16x8*>(yrow + (size_t)(16 * f + pp) * kCout + 8 * c) = v;
-#else
-                    if (v[0] == (__bf16)12345.f) yrow[0] = v[1];
-#endif
                 }
                 asm volatile("" ::: "memory");
             }
         }
-#ifdef MCGMIL_STEM_LATE_STAGE
-        if (more) stage(t + 1, cur ^ 1);
-#endif
         __syncthreads();
     }
 
