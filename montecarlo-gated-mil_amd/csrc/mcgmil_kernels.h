@@ -668,6 +668,8 @@ __global__ __launch_bounds__(kGateThreads) void gate_scores_kernel(const GatePar
 // softmax_pool_kernel: one 256-thread block per (t, bag). A = softmax over the bag's
 // instances (model.py:305), Y_c = sum_n A z_c (model.py:308-316).
 // ---------------------------------------------------------------------------------------
+constexpr int kSoftmaxRows = 16;    // register path for bags of up to 4096 instances
+
 __global__ __launch_bounds__(256) void softmax_pool_kernel(const int32_t* bag_off, int T, int C,
                                                            const float* logits, const float* zz,
                                                            float* Y, float* A) {
@@ -684,6 +686,51 @@ __global__ __launch_bounds__(256) void softmax_pool_kernel(const int32_t* bag_of
     const size_t R0 = (size_t)T * ob + (size_t)t * Nb;
     const size_t abase = (size_t)T * C * ob + (size_t)t * C * Nb;
     for (int c = 0; c < C; ++c) {
+        if (Nb <= 256 * kSoftmaxRows) {
+            // the bag's logits of class c stay in registers: one read of logits and z, one exp
+            // per row (same per-thread order and reduction tree as the streaming path below)
+            float e[kSoftmaxRows];
+            float m = -INFINITY;
+#pragma unroll
+            for (int k = 0; k < kSoftmaxRows; ++k) {
+                const int n = tid + 256 * k;
+                e[k] = n < Nb ? logits[(R0 + n) * C + c] : -INFINITY;
+                m = fmaxf(m, e[k]);
+            }
+            m = wave_max(m);
+            if (lane == 0) sred[0][wave] = m;
+            __syncthreads();
+            m = fmaxf(fmaxf(sred[0][0], sred[0][1]), fmaxf(sred[0][2], sred[0][3]));
+            __syncthreads();
+            float s = 0.f, y = 0.f;
+#pragma unroll
+            for (int k = 0; k < kSoftmaxRows; ++k) {
+                const int n = tid + 256 * k;
+                if (n < Nb) {
+                    e[k] = expf(e[k] - m);
+                    s += e[k];
+                    y = fmaf(e[k], zz[(R0 + n) * C + c], y);
+                }
+            }
+            s = wave_sum(s);
+            y = wave_sum(y);
+            if (lane == 0) { sred[0][wave] = s; sred[1][wave] = y; }
+            __syncthreads();
+            s = (sred[0][0] + sred[0][1]) + (sred[0][2] + sred[0][3]);
+            y = (sred[1][0] + sred[1][1]) + (sred[1][2] + sred[1][3]);
+            __syncthreads();
+            const float inv = 1.0f / s;
+            if (A) {
+                float* Ao = A + abase + (size_t)c * Nb;
+#pragma unroll
+                for (int k = 0; k < kSoftmaxRows; ++k) {
+                    const int n = tid + 256 * k;
+                    if (n < Nb) Ao[n] = e[k] * inv;
+                }
+            }
+            if (tid == 0) Yo[c] = y * inv;
+            continue;
+        }
         float m = -INFINITY;
         for (int n = tid; n < Nb; n += 256) m = fmaxf(m, logits[(R0 + n) * C + c]);
         m = wave_max(m);
@@ -736,7 +783,8 @@ __global__ __launch_bounds__(256) void bag_stats_kernel(const int32_t* bag_off, 
         const float* a = A + (size_t)T * C * ob + (size_t)c * Nb + n;
         const size_t step = (size_t)C * Nb;
         double s = 0.0, ss = 0.0;
-        for (int t = 0; t < T; ++t) {
+#pragma unroll 10
+        for (int t = 0; t < T; ++t) {     // unrolled: the strided loads overlap (same sum order)
             const double v = a[(size_t)t * step];
             s += v;
             ss += v * v;
