@@ -115,10 +115,33 @@ int cu_count() {
 
 // ---- BatchNorm statistics of the output (see the header comment)
 // Running sums of NCH channels of one lane: around x0 (the lane's first value per channel).
-template <int NCH>
+// PACK keeps the shifts as bf16 pairs (they are bf16 outputs, so exactly): half the registers.
+template <int NCH, bool PACK = false>
 struct LaneStats {
-    float x0[NCH], S[NCH], SS[NCH];
+    float x0f[PACK ? 1 : NCH];
+    uint32_t x0p[PACK ? NCH / 2 : 1];
+    float S[NCH], SS[NCH];
     float n;
+    __device__ __forceinline__ float x0(int c) const {
+        if constexpr (PACK) return __uint_as_float((c & 1) ? (x0p[c >> 1] & 0xFFFF0000u) : (x0p[c >> 1] << 16));
+        else return x0f[c];
+    }
+    __device__ __forceinline__ void set_x0(int c, float x) {
+        if constexpr (PACK) {
+            const uint32_t b = __float_as_uint(x) >> 16;       // x is a bf16 value: exact
+            x0p[c >> 1] = (c & 1) ? ((x0p[c >> 1] & 0xFFFFu) | (b << 16)) : ((x0p[c >> 1] & 0xFFFF0000u) | b);
+        } else {
+            x0f[c] = x;
+        }
+    }
+    __device__ __forceinline__ void init() {
+        n = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            S[c] = SS[c] = 0.f;
+            set_x0(c, 0.f);
+        }
+    }
 };
 
 // (n, m, M2) <- merge with (nb, mb, M2b) for every channel (the counts are shared by the channels)
@@ -140,15 +163,15 @@ __device__ __forceinline__ void chan_merge(float& n, float (&m)[NCH], float (&M2
 // (butterfly, the lane-0 result kept), then over the WGM waves that share channels (LDS, wave
 // order). Lane channel of index c = 4 i + v: chan0 + 16 i + 4 (lane >> 4) + v (local to the
 // workgroup's channel tile of width BN). Writes stats[(row * 3 + k) * Cout + col0 + local].
-template <int NCH, int WGM, int BN>
-__device__ void write_stats(const LaneStats<NCH>& st, int chan0, int wm, float* lds, float* stats,
+template <int NCH, int WGM, int BN, bool PACK>
+__device__ void write_stats(const LaneStats<NCH, PACK>& st, int chan0, int wm, float* lds, float* stats,
                             int row, int Cout, int col0) {
     const int lane = threadIdx.x & 63;
     float n = st.n, m[NCH], M2[NCH];
     const float rn = n > 0.f ? 1.f / n : 0.f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-        m[c] = st.x0[c] + st.S[c] * rn;
+        m[c] = st.x0(c) + st.S[c] * rn;
         M2[c] = fmaxf(st.SS[c] - st.S[c] * st.S[c] * rn, 0.f);
         if (!(n > 0.f)) m[c] = M2[c] = 0.f;
     }
@@ -189,9 +212,9 @@ __device__ void write_stats(const LaneStats<NCH>& st, int chan0, int wm, float* 
 
 // The epilogue of one pixel fragment: round to bf16, store 4 x 8 bytes, accumulate statistics.
 // PRED: pixels past M are neither stored nor counted (only the last tile can have them).
-template <int FI, bool STATS, bool PRED>
+template <int FI, bool STATS, bool PRED, bool PACK>
 __device__ __forceinline__ void store_fragment(const f32x4 (&acc)[FI], __bf16* dst, bool valid,
-                                               bool first, LaneStats<4 * FI>& st) {
+                                               bool first, LaneStats<4 * FI, PACK>& st) {
     typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 #pragma unroll
     for (int i = 0; i < FI; ++i) {
@@ -203,8 +226,8 @@ __device__ __forceinline__ void store_fragment(const f32x4 (&acc)[FI], __bf16* d
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
                 const float x = (float)o[v];
-                if (first) st.x0[4 * i + v] = x;
-                float d = x - st.x0[4 * i + v];
+                if (first) st.set_x0(4 * i + v, x);
+                float d = x - st.x0(4 * i + v);
                 if (PRED) d = valid ? d : 0.f;
                 st.S[4 * i + v] += d;
                 st.SS[4 * i + v] = fmaf(d, d, st.SS[4 * i + v]);
@@ -293,11 +316,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
 #pragma unroll
         for (int i = 0; i < FI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     LaneStats<4 * FI> st;
-    if (STATS) {
-        st.n = 0.f;
-#pragma unroll
-        for (int c = 0; c < 4 * FI; ++c) st.x0[c] = st.S[c] = st.SS[c] = 0.f;
-    }
+    if (STATS) st.init();
 
     auto compute = [&](int buf) {
         const unsigned char* A = smem + buf * STAGE;
@@ -374,9 +393,8 @@ struct HaloGeom {
     int tiles;
 };
 
+template <bool STATS>
 __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom hg) {
-    constexpr bool STATS = false;   // measured: the statistics epilogue costs this kernel more than the
-                                    // separate statistics pass it saves (registers: 256 + spills)
     const ConvGeom& g = hg.g;
     constexpr int FI = 2, FJ = 4, KSTEPS = 18;          // wave: 64 pixels x 32 channels
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -397,12 +415,8 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
             const int co = wn * 32 + i * 16 + (lane & 15);
             wf[s][i] = *reinterpret_cast<const bf16x8*>(g.w + (size_t)co * 576 + s * 32 + (lane >> 4) * 8);
         }
-    LaneStats<4 * FI> st;
-    if (STATS) {
-        st.n = 0.f;
-#pragma unroll
-        for (int c = 0; c < 4 * FI; ++c) st.x0[c] = st.S[c] = st.SS[c] = 0.f;
-    }
+    LaneStats<4 * FI, true> st;   // bf16-pair shifts: this kernel is at the register limit
+    if (STATS) st.init();
 
     // No per-tile integer division on the vector side: a tile's first pixel (n0, oh0, ow0) is
     // scalar math, every lane-dependent offset below is split into (rows, cols) once per kernel
@@ -506,7 +520,8 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
         }
         buf ^= 1;
     }
-    (void)st;
+    if (STATS) write_stats<4 * FI, 4, 64>(st, wn * 32, wm, reinterpret_cast<float*>(smem), g.stats,
+                                          (int)blockIdx.x, 64, 0);
 }
 
 // ---- 3x3 / stride 1 / pad 1 with Cin = 64 k >= 128 and Cout % 128 == 0 (ResNet layers 2-4):
@@ -603,11 +618,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
 #pragma unroll
         for (int i = 0; i < FI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     LaneStats<4 * FI> st;
-    if (STATS) {
-        st.n = 0.f;
-#pragma unroll
-        for (int c = 0; c < 4 * FI; ++c) st.x0[c] = st.S[c] = st.SS[c] = 0.f;
-    }
+    if (STATS) st.init();
     int dqr[FJ];      // this lane's output pixel offset in the tile per fragment: rows << 16 | cols
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
@@ -756,7 +767,7 @@ Plan make_plan(ConvGeom& g) {
             hg.g = g;
             p.kind = 1;
             p.grid = g.Gm;
-            p.parts = 0;            // no statistics from this kernel (see conv3x3c64_kernel)
+            p.parts = g.Gm;
             p.lds = lds;
             p.hg = hg;
             return p;
@@ -812,7 +823,8 @@ int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
         raise_lds(conv_dma_kernel<128, true>);
         raise_lds(conv_dma_kernel<64, false>);
         raise_lds(conv_dma_kernel<64, true>);
-        raise_lds(conv3x3c64_kernel);
+        raise_lds(conv3x3c64_kernel<false>);
+        raise_lds(conv3x3c64_kernel<true>);
         raise_lds(conv3x3_halo_kernel<false>);
         raise_lds(conv3x3_halo_kernel<true>);
     });
@@ -821,7 +833,8 @@ int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
     if (p.kind == 1) {
         HaloGeom hg = p.hg;
         hg.g = g;
-        hipLaunchKernelGGL(conv3x3c64_kernel, grid, block, p.lds, s, hg);
+        if (stats) hipLaunchKernelGGL(conv3x3c64_kernel<true>, grid, block, p.lds, s, hg);
+        else hipLaunchKernelGGL(conv3x3c64_kernel<false>, grid, block, p.lds, s, hg);
     } else if (p.kind == 4) {
         HaloGeom hg = p.hg;
         hg.g = g;
