@@ -244,9 +244,10 @@ __device__ __forceinline__ void store_fragment(const f32x4 (&acc)[FI], __bf16* d
 // issued right after the barrier that opens step s (two compute phases to land; the next tile's
 // first stages load under this tile's last steps and epilogue); the wait is a counted vmcnt
 // before a raw s_barrier (a __syncthreads would drain the stage still in flight).
-template <int BN, bool STATS>
+template <int BM, int BN, int WGM, int NS, bool STATS>
 __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g) {
-    constexpr int BM = kBM, WGM = 4, WGN = 2;
+    constexpr int WGN = 8 / WGM;
+    constexpr bool PACK = BM * BN > kBM * 128;        // 128 x 64 wave tiles: bf16-pair shifts
     constexpr int STAGE = (BM + BN) * kRowBytes;
     constexpr int PA = BM / 64, PB = BN / 64;         // 1-KiB pieces per wave per stage (A, B)
     constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -272,7 +273,11 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
     }
     // A pieces: the pixel rows of the tile being fetched (the issue side runs two steps ahead)
     int itm = -1;
-    int pix_base[PA], ih0[PA], iw0[PA], cha[PA];
+    // per piece: the window origin as a pixel index (may be negative) and the origin (ih0, iw0) as
+    // two int16 halves for the bounds test; the source chunk of the lane's LDS slot is the same
+    // for every piece ((r >> 1) & 7 does not depend on j)
+    int org[PA], ohw[PA];
+    const int cha = ((lane & 7) ^ ((4 * wave + (lane >> 4)) & 7)) * 8;
     auto setup = [&](int tm) {
         itm = tm;
 #pragma unroll
@@ -283,10 +288,10 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
             const int n = mm / (g.OH * g.OW);
             const int rem = mm - n * g.OH * g.OW;
             const int oh = rem / g.OW, ow = rem - oh * g.OW;
-            pix_base[j] = n * g.H * g.W;
-            ih0[j] = m < g.M ? oh * g.stride - g.pad : -(1 << 28);   // rows past M load zeros
-            iw0[j] = ow * g.stride - g.pad;
-            cha[j] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;     // source chunk of this lane's LDS slot
+            const int ih0 = m < g.M ? oh * g.stride - g.pad : -16384;   // rows past M load zeros
+            const int iw0 = ow * g.stride - g.pad;
+            org[j] = n * g.H * g.W + ih0 * g.W + iw0;
+            ohw[j] = (ih0 << 16) | (iw0 & 0xFFFF);
         }
     };
     auto issue = [&](int step, int buf) {
@@ -294,14 +299,14 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
         if (tm != itm) setup(tm);
         const int khw = kt / g.cin_tiles, cc = kt - khw * g.cin_tiles;
         const int kh = khw / g.KW, kw = khw - kh * g.KW;
+        const int koff = kh * g.W + kw;
         unsigned char* A = smem + buf * STAGE;
         unsigned char* B = A + BM * kRowBytes;
 #pragma unroll
         for (int j = 0; j < PA; ++j) {
-            const int ih = ih0[j] + kh, iw = iw0[j] + kw;
+            const int ih = (ohw[j] >> 16) + kh, iw = (int)(short)(ohw[j] & 0xFFFF) + kw;
             const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-            const uint32_t off = ((uint32_t)(pix_base[j] + ih * g.W + iw) * (uint32_t)g.Cin +
-                                  (uint32_t)(cc * 64 + cha[j])) * 2u;
+            const uint32_t off = ((uint32_t)(org[j] + koff) * (uint32_t)g.Cin + (uint32_t)(cc * 64 + cha)) * 2u;
             dma16(xr, A + (wave + 8 * j) * 1024, ok ? off : 0x80000000u, 0);
         }
 #pragma unroll
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
     for (int j = 0; j < FJ; ++j)
 #pragma unroll
         for (int i = 0; i < FI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    LaneStats<4 * FI> st;
+    LaneStats<4 * FI, PACK> st;
     if (STATS) st.init();
 
     auto compute = [&](int buf) {
@@ -324,18 +329,23 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int kq = ks * 4 + (lane >> 4);
-            bf16x8 wf[FI], xf[FJ];
+            bf16x8 wf[FI];
 #pragma unroll
             for (int i = 0; i < FI; ++i)
                 wf[i] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WN + i * 16 + (lane & 15), kq));
+            // pixel fragments in groups of 4 (fewer live operand registers with 8 of them)
 #pragma unroll
-            for (int j = 0; j < FJ; ++j)
-                xf[j] = *reinterpret_cast<const bf16x8*>(A + swz(wm * WM + j * 16 + (lane & 15), kq));
+            for (int j0 = 0; j0 < FJ; j0 += 4) {
+                bf16x8 xf[4];
 #pragma unroll
-            for (int i = 0; i < FI; ++i)
+                for (int j = 0; j < 4; ++j)
+                    xf[j] = *reinterpret_cast<const bf16x8*>(A + swz(wm * WM + (j0 + j) * 16 + (lane & 15), kq));
 #pragma unroll
-                for (int j = 0; j < FJ; ++j)
-                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[j][i], 0, 0, 0);
+                for (int i = 0; i < FI; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[j0 + j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[j0 + j][i], 0, 0, 0);
+            }
         }
     };
     auto epilogue = [&](int tm, bool first) {
@@ -351,20 +361,21 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
         }
     };
 
+    // NS LDS stages: step s + NS - 1 is issued into the stage step s - 1 used
     if (steps > 0) {
         issue(0, 0);
-        if (steps > 1) issue(1, 1);
+        if (NS == 3 && steps > 1) issue(1, 1);
     }
     int buf = 0, kt = 0, tm = tm0;
     for (int s = 0; s < steps; ++s) {
         // step s landed (counted: the next step's DMAs may stay in flight; vmcnt retires in order)
-        if (s + 1 < steps) wait_vmcnt<PA + PB>();
+        if (NS == 3 && s + 1 < steps) wait_vmcnt<PA + PB>();
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (s + 2 < steps) issue(s + 2, buf == 0 ? kStages - 1 : buf - 1);
+        if (s + NS - 1 < steps) issue(s + NS - 1, buf == 0 ? NS - 1 : buf - 1);
         compute(buf);
-        buf = buf == kStages - 1 ? 0 : buf + 1;
+        buf = buf == NS - 1 ? 0 : buf + 1;
         if (++kt == g.KT) {
             epilogue(tm, tm == tm0);
             kt = 0;
@@ -718,7 +729,8 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
 
 // ---- launch plan: which kernel, its grid and the statistics rows (Gm x 3 x Cout floats)
 struct Plan {
-    int kind = 0;          // 1: halo 64 -> 64, 2: dma BN=128, 3: dma BN=64, 4: halo, streamed weights
+    int kind = 0;          // 1: halo 64 -> 64, 2: dma 256 x 128, 3: dma 256 x 64, 4: halo, streamed
+                           // weights, 5: dma 512 x 128, 6: dma 256 x 256
     int grid = 0;
     int parts = 0;         // statistics rows
     size_t lds = 0;
@@ -802,6 +814,28 @@ Plan make_plan(ConvGeom& g) {
     }
     if (gm < 1) gm = 1;
     if (gm > g.tiles_m) gm = g.tiles_m;
+    // 128 x 64 wave tiles (25% less LDS fragment traffic per MFMA than 64 x 64), two LDS stages:
+    // 256 x 256 when Cout % 256 == 0 (layer 3: +30-34%, layer 4: +7%, measured in one process);
+    // 512 x 128 measured slower on the 128-channel layer (kept for MCGMIL_CONV_TILE=big512);
+    // MCGMIL_CONV_TILE=small keeps 256 x 128
+    const bool small = force && !strcmp(force, "small");
+    const bool big512 = force && !strcmp(force, "big512");
+    if (!small && BN == 128 && (g.Cout % 256 == 0 || big512)) {
+        const int bm = g.Cout % 256 == 0 ? 256 : 512, bn = g.Cout % 256 == 0 ? 256 : 128;
+        g.tiles_m = (g.M + bm - 1) / bm;
+        g.tiles_n = g.Cout / bn;
+        int gb = cus / g.tiles_n;
+        if (gb < 1) gb = 1;
+        if (gb > g.tiles_m) gb = g.tiles_m;
+        g.Gm = gb;
+        p.kind = bn == 256 ? 6 : 5;
+        p.grid = g.tiles_n * gb;
+        // no statistics from these shapes: with them the kernel spills (256 VGPRs), and the separate
+        // statistics pass of a layer-3/4 activation (10-20 us) costs less than that
+        p.parts = 0;
+        p.lds = (size_t)2 * (bm + bn) * kRowBytes;
+        return p;
+    }
     g.Gm = gm;
     p.kind = BN == 128 ? 2 : 3;
     p.grid = g.tiles_n * gm;
@@ -819,10 +853,12 @@ void raise_lds(K k) {
 int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
     static std::once_flag once;
     std::call_once(once, [] {
-        raise_lds(conv_dma_kernel<128, false>);
-        raise_lds(conv_dma_kernel<128, true>);
-        raise_lds(conv_dma_kernel<64, false>);
-        raise_lds(conv_dma_kernel<64, true>);
+        raise_lds(conv_dma_kernel<256, 128, 4, 3, false>);
+        raise_lds(conv_dma_kernel<256, 128, 4, 3, true>);
+        raise_lds(conv_dma_kernel<256, 64, 4, 3, false>);
+        raise_lds(conv_dma_kernel<256, 64, 4, 3, true>);
+        raise_lds(conv_dma_kernel<512, 128, 4, 2, false>);
+        raise_lds(conv_dma_kernel<256, 256, 2, 2, false>);
         raise_lds(conv3x3c64_kernel<false>);
         raise_lds(conv3x3c64_kernel<true>);
         raise_lds(conv3x3_halo_kernel<false>);
@@ -841,11 +877,15 @@ int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
         if (stats) hipLaunchKernelGGL(conv3x3_halo_kernel<true>, grid, block, p.lds, s, hg);
         else hipLaunchKernelGGL(conv3x3_halo_kernel<false>, grid, block, p.lds, s, hg);
     } else if (p.kind == 2) {
-        if (stats) hipLaunchKernelGGL((conv_dma_kernel<128, true>), grid, block, p.lds, s, g);
-        else hipLaunchKernelGGL((conv_dma_kernel<128, false>), grid, block, p.lds, s, g);
+        if (stats) hipLaunchKernelGGL((conv_dma_kernel<256, 128, 4, 3, true>), grid, block, p.lds, s, g);
+        else hipLaunchKernelGGL((conv_dma_kernel<256, 128, 4, 3, false>), grid, block, p.lds, s, g);
+    } else if (p.kind == 5) {
+        hipLaunchKernelGGL((conv_dma_kernel<512, 128, 4, 2, false>), grid, block, p.lds, s, g);
+    } else if (p.kind == 6) {
+        hipLaunchKernelGGL((conv_dma_kernel<256, 256, 2, 2, false>), grid, block, p.lds, s, g);
     } else {
-        if (stats) hipLaunchKernelGGL((conv_dma_kernel<64, true>), grid, block, p.lds, s, g);
-        else hipLaunchKernelGGL((conv_dma_kernel<64, false>), grid, block, p.lds, s, g);
+        if (stats) hipLaunchKernelGGL((conv_dma_kernel<256, 64, 4, 3, true>), grid, block, p.lds, s, g);
+        else hipLaunchKernelGGL((conv_dma_kernel<256, 64, 4, 3, false>), grid, block, p.lds, s, g);
     }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "convolution kernel launch");
@@ -876,6 +916,8 @@ int validate(const mcgmil_conv_args* a) {
     if (a->kernel_h < 1 || a->kernel_w < 1 || a->kernel_h > 7 || a->kernel_w > 7)
         return fail(MCGMIL_E_UNSUPPORTED, "kernel size must be in 1..7");
     if (a->stride < 1 || a->pad < 0) return fail(MCGMIL_E_INVALID, "stride must be >= 1 and pad >= 0");
+    if (a->height > 16383 || a->width > 16383 || a->pad > 64)
+        return fail(MCGMIL_E_UNSUPPORTED, "height and width must be <= 16383 and pad <= 64");
     const long long oh = ((long long)a->height + 2 * a->pad - a->kernel_h) / a->stride + 1;
     const long long ow = ((long long)a->width + 2 * a->pad - a->kernel_w) / a->stride + 1;
     if (oh < 1 || ow < 1) return fail(MCGMIL_E_INVALID, "the kernel does not fit the padded input");
