@@ -291,7 +291,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
             const int ih0 = m < g.M ? oh * g.stride - g.pad : -16384;   // rows past M load zeros
             const int iw0 = ow * g.stride - g.pad;
             org[j] = n * g.H * g.W + ih0 * g.W + iw0;
-            ohw[j] = (ih0 << 16) | (iw0 & 0xFFFF);
+            ohw[j] = (int)(((uint32_t)ih0 << 16) | ((uint32_t)iw0 & 0xFFFFu));
         }
     };
     auto issue = [&](int step, int buf) {
