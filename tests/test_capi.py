@@ -134,3 +134,58 @@ def test_bn_workspace_size_and_validation(hip_lib):
     assert rc == -1 and b"running_var" in hip_lib.mcgmil_last_error()
     # a missing workspace is refused before anything is launched
     assert hip_lib.mcgmil_batchnorm_act(ctypes.byref(_bn()), None) == -4
+
+
+def _stem(**kw):
+    from mcgmil import _lib
+    a = _lib.StemArgs()
+    a.batch, a.in_channels, a.height, a.width = 4, 3, 224, 224
+    a.out_channels, a.kernel, a.stride, a.pad = 64, 7, 2, 3
+    a.pool_kernel, a.pool_stride, a.pool_pad, a.relu, a.eps = 3, 2, 1, 1, 1e-5
+    for k, v in kw.items():
+        setattr(a, k, v)
+    return a
+
+
+def test_stem_sizes_and_validation(hip_lib):
+    """mcgmil_stem_*: packed-weight and workspace queries (the workspace holds the 112 x 112 x 64
+    activation when pooling) and the shapes the kernel refuses (no launches)."""
+    n = ctypes.c_size_t()
+    assert hip_lib.mcgmil_stem_packed_size(ctypes.byref(_stem()), ctypes.byref(n)) == 0
+    assert n.value == 6 * 4 * 64 * 16                                  # 21 (ci, kh) rows -> 6 K steps
+    assert hip_lib.mcgmil_stem_workspace_size(ctypes.byref(_stem()), ctypes.byref(n)) == 0
+    assert n.value >= 4 * 112 * 112 * 64 * 2 and n.value % 256 == 0
+    n2 = ctypes.c_size_t()
+    assert hip_lib.mcgmil_stem_workspace_size(ctypes.byref(_stem(pool_kernel=0)), ctypes.byref(n2)) == 0
+    assert n2.value < 4 * 112 * 112 * 64 * 2                           # conv written into y directly
+    for k, v in {"in_channels": 5, "out_channels": 128, "stride": 1, "width": 223, "kernel": 9,
+                 "width_wide": 1000}.items():
+        a = _stem(width=1000) if k == "width_wide" else _stem(**{k: v})
+        assert hip_lib.mcgmil_stem_workspace_size(ctypes.byref(a), ctypes.byref(n)) == -2, k
+    assert hip_lib.mcgmil_stem_workspace_size(ctypes.byref(_stem(relu=3)), ctypes.byref(n)) == -1
+    assert hip_lib.mcgmil_stem_forward(ctypes.byref(_stem()), None) == -1   # NULL x / w / y
+
+
+def test_conv_stats_parts_and_validation(hip_lib):
+    """mcgmil_conv_stats_parts: one statistics row per workgroup row of the kernel the layer uses
+    (0 for the 256 x 256 shape), and the argument checks (no launches)."""
+    from mcgmil import _lib
+    p = ctypes.c_int32()
+
+    def conv(cin, cout, k, s, pad, hw=28, **kw):
+        a = _lib.ConvArgs()
+        a.batch, a.height, a.width, a.in_channels = 8, hw, hw, cin
+        a.out_channels, a.kernel_h, a.kernel_w, a.stride, a.pad = cout, k, k, s, pad
+        for key, v in kw.items():
+            setattr(a, key, v)
+        return a
+    assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 64, 3, 1, 1, 56)), ctypes.byref(p)) == 0
+    assert p.value >= 1                                                  # layer-1 halo kernel
+    assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 128, 3, 2, 1, 56)), ctypes.byref(p)) == 0
+    assert p.value >= 1
+    assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(256, 256, 3, 1, 1, 14)), ctypes.byref(p)) == 0
+    assert p.value == 0                                                  # 256 x 256 tiles
+    assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(48, 64, 3, 1, 1)), ctypes.byref(p)) == -2
+    assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 64, 3, 0, 1)), ctypes.byref(p)) == -1
+    assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 64, 3, 1, 1, 20000)), ctypes.byref(p)) == -2
+    assert hip_lib.mcgmil_conv2d(ctypes.byref(conv(64, 64, 3, 1, 1)), None) == -1   # NULL x / w / y
