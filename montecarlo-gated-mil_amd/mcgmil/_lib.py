@@ -121,7 +121,8 @@ _lib = None
 
 
 def lib_path() -> str:
-    return _build.LIB
+    # MCGMIL_LIB: an A/B build of the same library (timing studies); default the in-tree build
+    return os.environ.get("MCGMIL_LIB", _build.LIB)
 
 
 def load():
