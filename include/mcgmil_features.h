@@ -88,7 +88,7 @@ size_t mcgmil_bn_args_size(void);   /* sizeof(mcgmil_bn_args), for binding check
 typedef struct mcgmil_conv_args {
     int32_t batch, height, width, in_channels;
     int32_t out_channels, kernel_h, kernel_w, stride, pad;
-    int32_t reserved;
+    int32_t in_relu;            /* with in_ab: 1 = ReLU after the input BatchNorm, 0 = none */
     const void* x;              /* bf16 [batch, height, width, in_channels] */
     const void* w;              /* packed bf16 [out_channels, kernel_h, kernel_w, in_channels] */
     void* y;                    /* bf16 [batch, OH, OW, out_channels] */
@@ -98,6 +98,15 @@ typedef struct mcgmil_conv_args {
                                    kernel emits none: then stats is ignored and the BN computes
                                    its statistics from y); hand them to mcgmil_batchnorm_act as
                                    partials. NULL: not computed */
+    const float* in_ab;         /* optional [2][in_channels] fp32 input BatchNorm (a_c, then b_c,
+                                   as mcgmil_batchnorm_coefficients writes them): the convolution
+                                   reads bf16(max(fmaf(x, a_c, b_c), 0)) (in_relu; without it
+                                   bf16(fmaf(x, a_c, b_c))) in place of every in-image x, padding
+                                   staying zero -- conv(relu(bn(x))) bit-identical to
+                                   mcgmil_batchnorm_act followed by mcgmil_conv2d, without
+                                   writing and re-reading bn(x). Only where
+                                   mcgmil_conv_input_bn() reports support (the 3x3 / stride 1 halo
+                                   kernels), else MCGMIL_E_UNSUPPORTED. NULL: x as is */
 } mcgmil_conv_args;
 
 size_t mcgmil_conv_args_size(void);
@@ -143,9 +152,18 @@ int mcgmil_pack_stem_weights(const mcgmil_stem_args* a, const void* weight, int3
 int mcgmil_stem_workspace_size(const mcgmil_stem_args* a, size_t* bytes);
 int mcgmil_stem_forward(const mcgmil_stem_args* a, void* stream);
 int mcgmil_conv_stats_parts(const mcgmil_conv_args* a, int32_t* parts);
+/* *supported = 1 when mcgmil_conv2d accepts in_ab for this geometry (in_ab itself not read) */
+int mcgmil_conv_input_bn(const mcgmil_conv_args* a, int32_t* supported);
 int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream);
 int mcgmil_bn_workspace_size(const mcgmil_bn_args* a, size_t* bytes);
 int mcgmil_batchnorm_act(const mcgmil_bn_args* a, void* stream);
+/* The per-channel coefficients mcgmil_batchnorm_act would apply, without the apply pass:
+ * ab[c] = a_c = gamma_c / sqrt(var_c + eps), ab[C + c] = b_c = beta_c - mean_c * a_c (fp32,
+ * [2][C], 4-byte aligned). Statistics as mcgmil_batchnorm_act: from partials, from the running
+ * statistics, or from a pass over x (then workspace as mcgmil_bn_workspace_size). y, residual and
+ * the pooling fields are ignored; batch_mean / batch_invstd are written when given. For a consumer
+ * that applies the BatchNorm itself (mcgmil_conv_args.in_ab). */
+int mcgmil_batchnorm_coefficients(const mcgmil_bn_args* a, float* ab, void* stream);
 
 #ifdef __cplusplus
 }

@@ -433,26 +433,37 @@ int apply_step(const mcgmil_bn_args* a, const float* ab, hipStream_t s) {
 
 // finalize (statistics from `parts` partial sums around the per-channel shift row `shift`, or
 // the running statistics) then the normalise / pool pass; ab lives at the workspace start
+// ab_out: write a, b there and stop (mcgmil_batchnorm_coefficients); NULL: a, b at the workspace
+// start, then the apply / pool pass
 template <typename E>
-int finish(const mcgmil_bn_args* a, const float* part, int parts, const E* shift, hipStream_t s) {
+int finish(const mcgmil_bn_args* a, const float* part, int parts, const E* shift, hipStream_t s,
+           float* ab_out = nullptr) {
     const int C = a->channels;
-    float* ab = static_cast<float*>(a->workspace);   // [2][C]
+    float* ab = ab_out ? ab_out : static_cast<float*>(a->workspace);   // [2][C]
     hipLaunchKernelGGL(bn_finalize_kernel<E>, dim3((C + kFinCh - 1) / kFinCh), dim3(kThreads), 0, s, part, parts, a->rows,
                        C, shift, a->gamma, a->beta, a->running_mean, a->running_var, a->eps, ab,
                        a->batch_mean, a->batch_invstd);
+    if (ab_out) {
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "batchnorm finalize launch");
+    }
     return apply_step<E>(a, ab, s);
 }
 
 template <typename E>
-int run(const mcgmil_bn_args* a, hipStream_t s) {
+int run(const mcgmil_bn_args* a, hipStream_t s, float* ab_out = nullptr) {
     const int C = a->channels;
     float* part = static_cast<float*>(a->workspace) + 2 * C;   // [parts][2][C]
     const E* x = static_cast<const E*>(a->x);
     if (!a->running_mean && a->partials) {       // statistics from the producer's (n, mean, M2)
-        float* ab = static_cast<float*>(a->workspace);
+        float* ab = ab_out ? ab_out : static_cast<float*>(a->workspace);
         hipLaunchKernelGGL(bn_finalize_chan_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kThreads), 0, s,
                            a->partials, a->num_partials, C, a->gamma, a->beta, a->eps, ab, a->batch_mean,
                            a->batch_invstd);
+        if (ab_out) {
+            const hipError_t e = hipGetLastError();
+            return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "batchnorm finalize launch");
+        }
         return apply_step<E>(a, ab, s);
     }
     int parts = 0;
@@ -461,7 +472,7 @@ int run(const mcgmil_bn_args* a, hipStream_t s) {
         const long long rpp = (a->rows + parts - 1) / parts;
         hipLaunchKernelGGL(bn_partial_kernel<E>, dim3(parts), dim3(kThreads), 0, s, x, a->rows, C, rpp, part);
     }
-    return finish<E>(a, part, parts, x, s);   // shift row: x[0, :]
+    return finish<E>(a, part, parts, x, s, ab_out);   // shift row: x[0, :]
 }
 
 }  // namespace
@@ -502,6 +513,28 @@ int mcgmil_batchnorm_act(const mcgmil_bn_args* a, void* stream) {
                                         "mcgmil_bn_workspace_size()");
     hipStream_t s = static_cast<hipStream_t>(stream);
     return a->dtype == MCGMIL_BF16 ? run<__bf16>(a, s) : run<float>(a, s);
+}
+
+int mcgmil_batchnorm_coefficients(const mcgmil_bn_args* a, float* ab, void* stream) {
+    if (!a) return fail(MCGMIL_E_INVALID, "mcgmil_bn_args is NULL");
+    if (!ab || ((uintptr_t)ab & 3)) return fail(MCGMIL_E_INVALID, "ab must be a 4-byte aligned [2][C] buffer");
+    // the apply-side fields do not matter here: validate the rest as mcgmil_batchnorm_act would
+    mcgmil_bn_args b = *a;
+    b.residual = nullptr;
+    b.pool_kernel = 0;
+    b.relu = 0;
+    // x is only read by the statistics pass; y never (a placeholder keeps validate() generic)
+    void* const placeholder = reinterpret_cast<void*>(static_cast<uintptr_t>(256));
+    b.y = b.x ? const_cast<void*>(b.x) : placeholder;
+    if (!b.x) b.x = placeholder;
+    if (int rc = validate(&b)) return rc;
+    const bool pass = !b.running_mean && !b.partials;     // statistics from a pass over x
+    if (pass && !a->x) return fail(MCGMIL_E_INVALID, "batch statistics without partials need x");
+    if (pass && (!b.workspace || b.workspace_bytes < ws_bytes(&b) || ((uintptr_t)b.workspace & 255)))
+        return fail(MCGMIL_E_WORKSPACE, "workspace missing, misaligned or smaller than "
+                                        "mcgmil_bn_workspace_size()");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    return b.dtype == MCGMIL_BF16 ? run<__bf16>(&b, s, ab) : run<float>(&b, s, ab);
 }
 
 }  // extern "C"

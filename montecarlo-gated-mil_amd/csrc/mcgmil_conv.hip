@@ -59,6 +59,8 @@ struct ConvGeom {
     const __bf16* w;
     __bf16* y;
     float* stats;        // [Gm][3][Cout] (count, mean, M2) per workgroup row, or NULL
+    const float* in_ab;  // [2][Cin] input BatchNorm (a_c then b_c; halo kernels only), or NULL
+    float in_lo;         // input BatchNorm floor: 0 (ReLU) or -inf
     int N, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad;
     int M;               // N * OH * OW (< 2^31, host-checked)
     int KT;              // K tiles: KH * KW * Cin / 64
@@ -97,6 +99,67 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint3
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// ---- Input BatchNorm (mcgmil_conv_args.in_ab) on a halo patch, in place. A lane rewrites the
+// 16-byte LDS slot it DMA'd itself (so only its own vmcnt has to cover the DMA, no barrier):
+// the 8 channels become bf16(max(fmaf(x, a_c, b_c), lo)) -- mcgmil_batchnorm_act's apply
+// arithmetic, so the convolution sees bit-identical inputs to the unfused pair of passes. keep is
+// 0 for padding pixels, which must stay zero (BN(0) = b_c is not).
+// The LDS read and write are inline asm: the compiler's wait-count pass treats a ds_read after
+// an LDS-DMA as a possible alias and would put an s_waitcnt vmcnt(0) in front of it, draining
+// the weight and patch DMAs just issued for the next step. The slot's own DMA is covered by the
+// caller's counted wait; the caller also waits for the writes (wait_lds_writes) before the
+// barrier that publishes the patch.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t lds_addr(const unsigned char* p) {
+    return (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const unsigned char*)p);
+}
+__device__ __forceinline__ u32x4 bn_values(u32x4 u, const float (&a)[8], const float (&b)[8], float lo, bool keep) {
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        o[2 * j] = (__bf16)fmaxf(fmaf(__uint_as_float(u[j] << 16), a[2 * j], b[2 * j]), lo);
+        o[2 * j + 1] = (__bf16)fmaxf(fmaf(__uint_as_float(u[j] & 0xFFFF0000u), a[2 * j + 1], b[2 * j + 1]), lo);
+    }
+    return __builtin_bit_cast(u32x4, o) & (keep ? 0xFFFFFFFFu : 0u);
+}
+__device__ __forceinline__ void bn_slot(unsigned char* slot, const float (&a)[8], const float (&b)[8], float lo,
+                                        bool keep) {
+    const uint32_t addr = lds_addr(slot);
+    u32x4 u;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(u) : "v"(addr) : "memory");
+    const u32x4 r = bn_values(u, a, b, lo, keep);
+    asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(r) : "memory");
+}
+// Four slots at once (one LDS round trip instead of four); slots past `count` are read (at a
+// valid address) but not written. The wait names the read values, so no use moves above it.
+__device__ __forceinline__ void bn_slots4(const uint32_t (&addr)[4], int count, uint32_t keep_bits,
+                                          const float (&a)[8], const float (&b)[8], float lo) {
+    u32x4 u0, u1, u2, u3;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(u0) : "v"(addr[0]) : "memory");
+    asm volatile("ds_read_b128 %0, %1" : "=v"(u1) : "v"(addr[1]) : "memory");
+    asm volatile("ds_read_b128 %0, %1" : "=v"(u2) : "v"(addr[2]) : "memory");
+    asm volatile("ds_read_b128 %0, %1" : "=v"(u3) : "v"(addr[3]) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3)::"memory");
+    const u32x4 r0 = bn_values(u0, a, b, lo, keep_bits & 1);
+    asm volatile("ds_write_b128 %0, %1" ::"v"(addr[0]), "v"(r0) : "memory");
+    if (count > 1) {
+        const u32x4 r1 = bn_values(u1, a, b, lo, (keep_bits >> 1) & 1);
+        asm volatile("ds_write_b128 %0, %1" ::"v"(addr[1]), "v"(r1) : "memory");
+    }
+    if (count > 2) {
+        const u32x4 r2 = bn_values(u2, a, b, lo, (keep_bits >> 2) & 1);
+        asm volatile("ds_write_b128 %0, %1" ::"v"(addr[2]), "v"(r2) : "memory");
+    }
+    if (count > 3) {
+        const u32x4 r3 = bn_values(u3, a, b, lo, (keep_bits >> 3) & 1);
+        asm volatile("ds_write_b128 %0, %1" ::"v"(addr[3]), "v"(r3) : "memory");
+    }
+}
+
+__device__ __forceinline__ void wait_lds_writes() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 int cu_count() {
@@ -404,7 +467,11 @@ struct HaloGeom {
     int tiles;
 };
 
-template <bool STATS>
+// With XF (input BatchNorm) the [2][64] a, b table sits after the two patches; each lane rewrites
+// its own slots of a tile's patch between its vmcnt wait and the barrier that opens the tile. A
+// lane's slots all hold one 8-channel chunk: pieces of a wave are wave + 8 k, so the swizzle
+// (p >> 1) & 7 of its pixels p = 8 piece + lane / 8 only depends on the wave's parity.
+template <bool STATS, bool XF>
 __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom hg) {
     const ConvGeom& g = hg.g;
     constexpr int FI = 2, FJ = 4, KSTEPS = 18;          // wave: 64 pixels x 32 channels
@@ -442,6 +509,12 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
     const int p0 = wave * 8 + (lane >> 3);       // first patch pixel this lane DMAs
     const int rr0 = p0 / WP, col0 = p0 - rr0 * WP;
     const int qstep = 64 / WP, rstep = 64 - qstep * WP;  // pieces advance by 64 patch pixels
+    uint32_t okm = 0;     // XF: bit k = piece k of this wave's in-flight patch is inside the image
+    float* ab_tbl = reinterpret_cast<float*>(smem + 2 * patch_bytes);
+    if (XF) {
+        if (threadIdx.x < 128) ab_tbl[threadIdx.x] = g.in_ab[threadIdx.x < 64 ? threadIdx.x : g.Cin + threadIdx.x - 64];
+        __syncthreads();
+    }
 
     auto issue = [&](int tile, int buf) {
         const int m0 = tile * kBM;
@@ -453,11 +526,13 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
             ++n;
         }
         unsigned char* Lp = smem + buf * patch_bytes;
-        for (int piece = wave; piece * 8 < hg.patch_px; piece += 8) {
+        okm = 0;
+        for (int piece = wave, k = 0; piece * 8 < hg.patch_px; piece += 8, ++k) {
             const int p = piece * 8 + (lane >> 3);
             const int c = (lane & 7) ^ ((p >> 1) & 7);     // source chunk of this lane's slot
             const int ih = prel - 1, iw = col - 1;
             const bool ok = n < g.N && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+            if (XF) okm |= (uint32_t)ok << k;
             const uint32_t off = ((uint32_t)((n * g.H + ih) * g.W + iw) * 64u + (uint32_t)c * 8u) * 2u;
             dma16(xr, Lp + piece * 1024, ok ? off : 0x80000000u, 0);
             col += rstep;
@@ -477,7 +552,27 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
     int buf = 0;
     for (int t = t0; t < t1; ++t) {
         // patch t landed; only the previous tile's epilogue stores (FI * FJ per lane) may still fly
-        wait_vmcnt<FI * FJ>();
+        if (t == t0) wait_vmcnt<0>();
+        else wait_vmcnt<FI * FJ>();
+        if (XF) {
+            const int c = (lane & 7) ^ ((4 * (wave & 1) + (lane >> 4)) & 7);
+            float a[8], b[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                a[j] = ab_tbl[8 * c + j];
+                b[j] = ab_tbl[64 + 8 * c + j];
+            }
+            // this wave's pieces wave + 8 k, four per LDS round trip
+            const uint32_t base = lds_addr(smem + buf * patch_bytes) + lane * 16 + wave * 1024;
+            const int np = (hg.patch_px / 8 - wave + 7) / 8;
+            for (int k0 = 0; k0 < np; k0 += 4) {
+                uint32_t ad[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) ad[j] = base + (uint32_t)(k0 + j < np ? k0 + j : k0) * 8192u;
+                bn_slots4(ad, np - k0, okm >> k0, a, b, g.in_lo);
+            }
+            wait_lds_writes();
+        }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (t + 1 < t1) issue(t + 1, buf ^ 1);
@@ -542,15 +637,21 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
 // streamed (~23 KB per step). Steps run tile-major, then cc, then tap; one barrier per step:
 //  - weights of step s + 1 go into the other of two 16-KB stages right after the barrier of s;
 //  - the patch of the NEXT (tile, cc) is loaded one 1-KiB piece per wave per tap (taps 0..7),
-//    issued after that step's weights, into the other of two 64-KB patch buffers (fixed 512
-//    pixels; pieces past the patch read out of range, i.e. zeros, without memory traffic);
+//    issued after that step's weights, into the other of two 60-KB patch buffers (fixed 480
+//    pixels; pieces past the patch read out of range, i.e. zeros, without memory traffic; the
+//    four pieces past the buffer are not issued);
 //  - so the wait at the top of step s is vmcnt(1) after a patch piece, vmcnt(FI * FJ) after a
 //    tile's epilogue stores, else vmcnt(0) (vmcnt retires in order).
 // Workgroups are mapped like conv_dma_kernel (one channel tile each, contiguous pixel tiles), so
 // the BatchNorm statistics epilogue is the same.
-constexpr int kPatchPx = 512;
+constexpr int kPatchPx = 480;          // 2 patches + 2 weight stages + an 8-KB a, b table = 160 KB
 
-template <bool STATS>
+// With XF (input BatchNorm) a lane rewrites its own slot of patch piece k two steps after issuing
+// it (tap k + 2, when the counted wait has covered it), piece 7 and the kernel's first patch
+// between the wait and the barrier that opens the patch's first step. A lane's slots of one patch
+// all hold one 8-channel chunk (see conv3x3c64_kernel), so its 8 a / 8 b values are loaded once
+// per patch.
+template <bool STATS, bool XF>
 __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeom hg) {
     const ConvGeom& g = hg.g;
     constexpr int BN = 128, WGM = 4, WGN = 2, WM = 64, WN = 64, FI = 4, FJ = 4;
@@ -569,6 +670,11 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
     const int HP = g.H + 2, WP = hg.WP, OHW = g.OH * g.OW;
     unsigned char* patch0 = smem;                        // [2][kPatchPx][128 B]
     unsigned char* wst0 = smem + 2 * PATCH;              // [2][BN][128 B]
+    float* ab_tbl = reinterpret_cast<float*>(wst0 + 2 * WSTAGE);   // XF: [2][Cin] a, b
+    if (XF) {
+        for (int i = threadIdx.x; i < 2 * g.Cin; i += kThreads) ab_tbl[i] = g.in_ab[i];
+        __syncthreads();
+    }
 
     // weights: 2 pieces per wave per step (rows 8 (wave + 8 j) + lane / 8 of the channel tile)
     const uint32_t K = (uint32_t)(9 * g.Cin);
@@ -591,6 +697,9 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
     const int qstep = 64 / WP, rstep = 64 - qstep * WP;
     int pn = 0, prel = 0, pcol = 0, pcc = 0;
     unsigned char* pdst = patch0;
+    uint32_t okm = 0;                   // XF: bit k = piece k of the patch being loaded is in the image
+    float xa[8], xb[8];                 // XF: a, b of this lane's chunk of that patch
+    const int xchunk = (lane & 7) ^ ((4 * (wave & 1) + (lane >> 4)) & 7);
     auto patch_begin = [&](int tm, int cc, int buf) {
         const int m0 = tm * kBM;
         pn = m0 / OHW;
@@ -602,12 +711,27 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
         }
         pcc = cc;
         pdst = patch0 + buf * PATCH;
+        if (XF) {
+            okm = 0;
+            const float* ab = ab_tbl + cc * 64 + xchunk * 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                xa[j] = ab[j];
+                xb[j] = ab[g.Cin + j];
+            }
+        }
     };
-    auto patch_piece = [&](int k) {
+    auto xform = [&](int k) {
+        if (8 * (wave + 8 * k) >= kPatchPx) return;
+        bn_slot(pdst + (wave + 8 * k) * 1024 + lane * 16, xa, xb, g.in_lo, (okm >> k) & 1);
+    };
+    auto patch_piece = [&](int k) -> bool {
+        if (8 * (wave + 8 * k) >= kPatchPx) return false;    // wave-uniform: past the buffer
         const int p = 8 * (wave + 8 * k) + (lane >> 3);
         const int c = (lane & 7) ^ ((p >> 1) & 7);
         const int ih = prel - 1, iw = pcol - 1;
         const bool ok = p < hg.patch_px && pn < g.N && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        if (XF) okm |= (uint32_t)ok << k;
         const uint32_t off = ((uint32_t)((pn * g.H + ih) * g.W + iw) * (uint32_t)g.Cin +
                               (uint32_t)(pcc * 64 + c * 8)) * 2u;
         dma16(xr, pdst + (wave + 8 * k) * 1024, ok ? off : 0x80000000u, 0);
@@ -621,6 +745,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
             prel -= HP;
             ++pn;
         }
+        return true;
     };
 
     f32x4 acc[FJ][FI];
@@ -669,9 +794,18 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
         if (wait_kind == 1) wait_vmcnt<1>();
         else if (wait_kind == 2) wait_vmcnt<FI * FJ>();
         else wait_vmcnt<0>();
+        const int cc = r / 9, tap = r - cc * 9;
+        if (XF && tap == 0) {       // this step opens a patch: the rest of this lane's slots
+            if (s == 0) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) xform(k);
+            } else {
+                xform(7);
+            }
+            wait_lds_writes();
+        }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        const int cc = r / 9, tap = r - cc * 9;
         wait_kind = 0;
         if (s + 1 < steps) issue_w(s + 1, (s + 1) & 1);
         // the next (tile, cc) patch: begun at tap 0, one piece per tap 0..7
@@ -681,8 +815,9 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
                 if (cc + 1 < CC) patch_begin(tm, cc + 1, pbuf ^ 1);
                 else patch_begin(tm + 1, 0, pbuf ^ 1);
             }
-            patch_piece(tap);
-            wait_kind = 1;
+            // vmcnt(1) at the next step leaves only this piece in flight; without a piece the
+            // weights just issued must land: vmcnt(0)
+            if (patch_piece(tap)) wait_kind = 1;
         }
         // compute step s: A from the patch at the tap offset, B from the weight stage
         {
@@ -705,6 +840,8 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
                         acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[j][i], 0, 0, 0);
             }
         }
+        // XF: piece tap - 2 of the patch being loaded has landed (the wait above retired it)
+        if (XF && more_patch && tap >= 2) xform(tap - 2);
         if (tap == 8) pbuf ^= 1;                        // next cc (or tile) uses the other patch
         if (++r == SPT) {
             const bool full = (tm + 1) * kBM <= g.M, first = tm == tm0;
@@ -743,6 +880,8 @@ ConvGeom geom_of(const mcgmil_conv_args* a) {
     g.w = static_cast<const __bf16*>(a->w);
     g.y = static_cast<__bf16*>(a->y);
     g.stats = a->stats;
+    g.in_ab = a->in_ab;
+    g.in_lo = a->in_relu ? 0.f : -INFINITY;
     g.N = a->batch; g.H = a->height; g.W = a->width; g.Cin = a->in_channels;
     g.Cout = a->out_channels; g.KH = a->kernel_h; g.KW = a->kernel_w;
     g.stride = a->stride; g.pad = a->pad;
@@ -771,7 +910,7 @@ Plan make_plan(ConvGeom& g) {
         const int imgs = (kBM - 1 + g.OH * g.OW - 1) / (g.OH * g.OW) + 1;
         hg.NR = rows + 2 + 2 * (imgs - 1);
         hg.patch_px = (hg.NR * hg.WP + 7) / 8 * 8;
-        const size_t lds = (size_t)2 * hg.patch_px * kRowBytes;
+        const size_t lds = (size_t)2 * hg.patch_px * kRowBytes + (g.in_ab ? 512 : 0);
         if (lds <= 160 * 1024) {
             hg.tiles = g.tiles_m;
             g.tiles_n = 1;
@@ -800,14 +939,15 @@ Plan make_plan(ConvGeom& g) {
         const int imgs = (kBM - 1 + g.OH * g.OW - 1) / (g.OH * g.OW) + 1;
         hg.NR = rows + 2 + 2 * (imgs - 1);
         hg.patch_px = hg.NR * hg.WP;
-        if (hg.patch_px <= kPatchPx) {
+        if (hg.patch_px <= kPatchPx && (!g.in_ab || g.Cin <= 1024)) {
             hg.tiles = g.tiles_m;
             g.Gm = gm;
             hg.g = g;
             p.kind = 4;
             p.grid = g.tiles_n * gm;
             p.parts = gm;
-            p.lds = (size_t)2 * kPatchPx * kRowBytes + (size_t)2 * 128 * kRowBytes;
+            p.lds = (size_t)2 * kPatchPx * kRowBytes + (size_t)2 * 128 * kRowBytes +
+                    (g.in_ab ? (size_t)8 * g.Cin : 0);
             p.hg = hg;
             return p;
         }
@@ -859,23 +999,29 @@ int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
         raise_lds(conv_dma_kernel<256, 64, 4, 3, true>);
         raise_lds(conv_dma_kernel<512, 128, 4, 2, false>);
         raise_lds(conv_dma_kernel<256, 256, 2, 2, false>);
-        raise_lds(conv3x3c64_kernel<false>);
-        raise_lds(conv3x3c64_kernel<true>);
-        raise_lds(conv3x3_halo_kernel<false>);
-        raise_lds(conv3x3_halo_kernel<true>);
+        raise_lds(conv3x3c64_kernel<false, false>);
+        raise_lds(conv3x3c64_kernel<true, false>);
+        raise_lds(conv3x3c64_kernel<false, true>);
+        raise_lds(conv3x3c64_kernel<true, true>);
+        raise_lds(conv3x3_halo_kernel<false, false>);
+        raise_lds(conv3x3_halo_kernel<true, false>);
+        raise_lds(conv3x3_halo_kernel<false, true>);
+        raise_lds(conv3x3_halo_kernel<true, true>);
     });
-    const bool stats = g.stats != nullptr;
+    const bool stats = g.stats != nullptr, xf = g.in_ab != nullptr;
     const dim3 grid((unsigned)p.grid), block(kThreads);
     if (p.kind == 1) {
         HaloGeom hg = p.hg;
         hg.g = g;
-        if (stats) hipLaunchKernelGGL(conv3x3c64_kernel<true>, grid, block, p.lds, s, hg);
-        else hipLaunchKernelGGL(conv3x3c64_kernel<false>, grid, block, p.lds, s, hg);
+        auto k = stats ? (xf ? conv3x3c64_kernel<true, true> : conv3x3c64_kernel<true, false>)
+                       : (xf ? conv3x3c64_kernel<false, true> : conv3x3c64_kernel<false, false>);
+        hipLaunchKernelGGL(k, grid, block, p.lds, s, hg);
     } else if (p.kind == 4) {
         HaloGeom hg = p.hg;
         hg.g = g;
-        if (stats) hipLaunchKernelGGL(conv3x3_halo_kernel<true>, grid, block, p.lds, s, hg);
-        else hipLaunchKernelGGL(conv3x3_halo_kernel<false>, grid, block, p.lds, s, hg);
+        auto k = stats ? (xf ? conv3x3_halo_kernel<true, true> : conv3x3_halo_kernel<true, false>)
+                       : (xf ? conv3x3_halo_kernel<false, true> : conv3x3_halo_kernel<false, false>);
+        hipLaunchKernelGGL(k, grid, block, p.lds, s, hg);
     } else if (p.kind == 2) {
         if (stats) hipLaunchKernelGGL((conv_dma_kernel<256, 128, 4, 3, true>), grid, block, p.lds, s, g);
         else hipLaunchKernelGGL((conv_dma_kernel<256, 128, 4, 3, false>), grid, block, p.lds, s, g);
@@ -916,6 +1062,7 @@ int validate(const mcgmil_conv_args* a) {
     if (a->kernel_h < 1 || a->kernel_w < 1 || a->kernel_h > 7 || a->kernel_w > 7)
         return fail(MCGMIL_E_UNSUPPORTED, "kernel size must be in 1..7");
     if (a->stride < 1 || a->pad < 0) return fail(MCGMIL_E_INVALID, "stride must be >= 1 and pad >= 0");
+    if (a->in_relu != 0 && a->in_relu != 1) return fail(MCGMIL_E_INVALID, "in_relu must be 0 or 1");
     if (a->height > 16383 || a->width > 16383 || a->pad > 64)
         return fail(MCGMIL_E_UNSUPPORTED, "height and width must be <= 16383 and pad <= 64");
     const long long oh = ((long long)a->height + 2 * a->pad - a->kernel_h) / a->stride + 1;
@@ -957,6 +1104,18 @@ int mcgmil_pack_conv_weights(const mcgmil_conv_args* a, const void* weight, int3
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "pack_conv_weights_kernel launch");
 }
 
+int mcgmil_conv_input_bn(const mcgmil_conv_args* a, int32_t* supported) {
+    int rc = validate(a);
+    if (rc) return rc;
+    if (!supported) return fail(MCGMIL_E_INVALID, "supported is NULL");
+    mcgmil_conv_args b = *a;
+    b.in_ab = reinterpret_cast<const float*>(16);   // a plan with the input BatchNorm
+    ConvGeom g = geom_of(&b);
+    const int kind = make_plan(g).kind;
+    *supported = kind == 1 || kind == 4;
+    return MCGMIL_OK;
+}
+
 int mcgmil_conv_stats_parts(const mcgmil_conv_args* a, int32_t* parts) {
     int rc = validate(a);
     if (rc) return rc;
@@ -973,8 +1132,12 @@ int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream) {
     if (((uintptr_t)a->x | (uintptr_t)a->w | (uintptr_t)a->y) & 15u)
         return fail(MCGMIL_E_ALIGN, "x, w and y must be 16-byte aligned");
     if ((uintptr_t)a->stats & 3u) return fail(MCGMIL_E_ALIGN, "stats must be 4-byte aligned");
+    if ((uintptr_t)a->in_ab & 3u) return fail(MCGMIL_E_ALIGN, "in_ab must be 4-byte aligned");
     ConvGeom g = geom_of(a);
     const Plan p = make_plan(g);
+    if (a->in_ab && p.kind != 1 && p.kind != 4)
+        return fail(MCGMIL_E_UNSUPPORTED, "in_ab: this layer's kernel has no input BatchNorm "
+                                          "(see mcgmil_conv_input_bn)");
     return launch(g, p, reinterpret_cast<hipStream_t>(stream));
 }
 

@@ -28,6 +28,7 @@ EXPORTED = (
     "mcgmil_image_to_bag", "mcgmil_attention_maps", "mcgmil_reconstruct_image",
     # include/mcgmil_features.h
     "mcgmil_bn_args_size", "mcgmil_bn_workspace_size", "mcgmil_batchnorm_act",
+    "mcgmil_batchnorm_coefficients", "mcgmil_conv_input_bn",
     "mcgmil_conv_args_size", "mcgmil_pack_conv_weights", "mcgmil_conv_stats_parts", "mcgmil_conv2d",
     "mcgmil_stem_args_size", "mcgmil_stem_packed_size", "mcgmil_pack_stem_weights",
     "mcgmil_stem_workspace_size", "mcgmil_stem_forward",
@@ -80,8 +81,8 @@ class ConvArgs(ctypes.Structure):
         ("batch", ctypes.c_int32), ("height", ctypes.c_int32), ("width", ctypes.c_int32),
         ("in_channels", ctypes.c_int32), ("out_channels", ctypes.c_int32),
         ("kernel_h", ctypes.c_int32), ("kernel_w", ctypes.c_int32), ("stride", ctypes.c_int32),
-        ("pad", ctypes.c_int32), ("reserved", ctypes.c_int32),
-        ("x", _vp), ("w", _vp), ("y", _vp), ("stats", _vp),
+        ("pad", ctypes.c_int32), ("in_relu", ctypes.c_int32),
+        ("x", _vp), ("w", _vp), ("y", _vp), ("stats", _vp), ("in_ab", _vp),
     ]
 
 
@@ -170,12 +171,16 @@ def load():
     L.mcgmil_bn_workspace_size.restype = ctypes.c_int
     L.mcgmil_batchnorm_act.argtypes = [pb, _vp]
     L.mcgmil_batchnorm_act.restype = ctypes.c_int
+    L.mcgmil_batchnorm_coefficients.argtypes = [pb, _vp, _vp]
+    L.mcgmil_batchnorm_coefficients.restype = ctypes.c_int
     pc = ctypes.POINTER(ConvArgs)
     L.mcgmil_conv_args_size.restype = ctypes.c_size_t
     L.mcgmil_pack_conv_weights.argtypes = [pc, _vp, ctypes.c_int32, _vp, _vp]
     L.mcgmil_pack_conv_weights.restype = ctypes.c_int
     L.mcgmil_conv_stats_parts.argtypes = [pc, ctypes.POINTER(ctypes.c_int32)]
     L.mcgmil_conv_stats_parts.restype = ctypes.c_int
+    L.mcgmil_conv_input_bn.argtypes = [pc, ctypes.POINTER(ctypes.c_int32)]
+    L.mcgmil_conv_input_bn.restype = ctypes.c_int
     L.mcgmil_conv2d.argtypes = [pc, _vp]
     L.mcgmil_conv2d.restype = ctypes.c_int
     ps = ctypes.POINTER(StemArgs)

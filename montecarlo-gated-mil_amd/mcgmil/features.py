@@ -28,7 +28,7 @@ layers run); MCGMIL_NATIVE_STEM=0 switches it off.
 """
 import ctypes
 import os
-from typing import Optional
+from typing import NamedTuple, Optional
 
 import torch
 import torch.nn as nn
@@ -124,16 +124,34 @@ def packed_conv_weight(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     return packed
 
 
-def conv2d(conv: nn.Conv2d, x: torch.Tensor, stats: bool = False):
+def conv_input_bn(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """Whether conv2d(conv, x, in_ab=...) can apply an input BatchNorm inside the convolution
+    (mcgmil_conv_input_bn: the 3x3 / stride 1 halo kernels). MCGMIL_FUSE_INPUT_BN=0 disables it."""
+    if os.environ.get("MCGMIL_FUSE_INPUT_BN", "1") == "0":
+        return False
+    L = _lib.load()
+    ok = ctypes.c_int32()
+    _lib.check(L.mcgmil_conv_input_bn(ctypes.byref(_conv_args(conv, x)), ctypes.byref(ok)), "mcgmil_conv_input_bn")
+    return bool(ok.value)
+
+
+def conv2d(conv: nn.Conv2d, x: torch.Tensor, stats: bool = False,
+           in_ab: Optional[torch.Tensor] = None, in_relu: bool = True):
     """conv(x) for a channels-last bf16 activation (see conv_fusable) on the MFMA kernel; returns a
     channels-last bf16 tensor, or with stats=True (y, partials): the BatchNorm statistics of y
     as [parts, 3, Cout] (count, mean, M2) blocks for batchnorm_act(..., partials=...), or None
-    where the layer's kernel emits none (the 3x3 64 -> 64 halo kernel)."""
+    where the layer's kernel emits none (256 x 256 tiles). With in_ab ([2, Cin] fp32 from
+    batchnorm_coefficients) the convolution reads relu?(bn(x)) instead of x (conv_input_bn)."""
     if not conv_fusable(conv, x):
         raise ValueError("conv2d needs a CUDA channels-last bf16 activation, a bias-free groups=1 "
                          "convolution with 64k channels and no autograd (see conv_fusable)")
     L = _lib.load()
     a = _conv_args(conv, x)
+    if in_ab is not None:
+        if in_ab.shape != (2, a.in_channels) or in_ab.dtype != torch.float32 or \
+                in_ab.device != x.device or not in_ab.is_contiguous():
+            raise ValueError("in_ab must be a contiguous fp32 [2, in_channels] tensor on x's device")
+        a.in_ab, a.in_relu = ctypes.c_void_p(in_ab.data_ptr()), int(bool(in_relu))
     oh = (a.height + 2 * a.pad - a.kernel_h) // a.stride + 1
     ow = (a.width + 2 * a.pad - a.kernel_w) // a.stride + 1
     y = torch.empty((a.batch, a.out_channels, oh, ow), dtype=torch.bfloat16, device=x.device,
@@ -231,6 +249,45 @@ def batchnorm_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool,
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     _lib.check(L.mcgmil_batchnorm_act(ctypes.byref(a), stream), "mcgmil_batchnorm_act")
     return y
+
+
+def batchnorm_coefficients(x: torch.Tensor, bn: nn.BatchNorm2d,
+                           partials: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The [2, C] fp32 (a_c, b_c) that batchnorm_act(x, bn, ...) would apply
+    (mcgmil_batchnorm_coefficients), for a consumer that applies them itself (conv2d's in_ab)."""
+    if not fusable(x, bn, None):
+        raise ValueError("batchnorm_coefficients needs what batchnorm_act needs (see fusable)")
+    L = _lib.load()
+    dev = x.device
+    N, C, H, W = x.shape
+    use_batch = bn.training or bn.running_mean is None or bn.running_var is None
+    gamma = _f32(bn.weight, dev) if bn.affine else None
+    beta = _f32(bn.bias, dev) if bn.affine else None
+    rmean = None if use_batch else _f32(bn.running_mean, dev)
+    rvar = None if use_batch else _f32(bn.running_var, dev)
+    a = _lib.BnArgs()
+    a.rows, a.channels, a.dtype = N * H * W, C, _DT[x.dtype]
+    a.batch, a.height, a.width = N, H, W
+    p = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    a.x = p(x)
+    a.gamma, a.beta, a.running_mean, a.running_var = p(gamma), p(beta), p(rmean), p(rvar)
+    a.eps = float(bn.eps)
+    ws = None
+    if partials is not None and use_batch:
+        if partials.dim() != 3 or partials.shape[1:] != (3, C) or not partials.is_contiguous() or \
+                partials.dtype != torch.float32 or partials.device != dev:
+            raise ValueError("partials must be a contiguous fp32 [parts, 3, C] tensor on x's device")
+        a.partials, a.num_partials = p(partials), partials.shape[0]
+    elif use_batch:
+        n = ctypes.c_size_t()
+        a.y = a.x
+        _lib.check(L.mcgmil_bn_workspace_size(ctypes.byref(a), ctypes.byref(n)), "mcgmil_bn_workspace_size")
+        ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
+        a.workspace, a.workspace_bytes = p(ws), n.value
+    ab = torch.empty((2, C), dtype=torch.float32, device=dev)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    _lib.check(L.mcgmil_batchnorm_coefficients(ctypes.byref(a), p(ab), stream), "mcgmil_batchnorm_coefficients")
+    return ab
 
 
 def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool,
@@ -366,17 +423,49 @@ def run_stem(conv: nn.Module, bn: nn.Module, pool: Optional[nn.Module], x: torch
     return bn_act(bn, conv(x), True, pool=pool)
 
 
-def conv_bn_act(conv: nn.Module, bn: nn.Module, x: torch.Tensor, relu: bool,
-                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+class DeferredBN(NamedTuple):
+    """relu?(bn(y)) left unapplied: the next convolution applies it to its input (conv2d's
+    in_ab), so the activation is neither written nor read a second time."""
+    y: torch.Tensor
+    ab: torch.Tensor                    # [2, C] fp32 (a_c, b_c) from batchnorm_coefficients
+    relu: bool
+    bn: nn.BatchNorm2d
+    partials: Optional[torch.Tensor]    # the statistics ab came from (None: running statistics)
+
+    def materialise(self) -> torch.Tensor:
+        return batchnorm_act(self.y, self.bn, self.relu, partials=self.partials)
+
+
+def _use_batch(bn: nn.BatchNorm2d) -> bool:
+    return bn.training or bn.running_mean is None or bn.running_var is None
+
+
+def conv_bn_act(conv: nn.Module, bn: nn.Module, x, relu: bool,
+                residual: Optional[torch.Tensor] = None, consumer: Optional[nn.Module] = None):
     """The blocks' `relu?(bn(conv(x)) [+ residual])`: on the GPU the MFMA convolution also emits
     the BatchNorm batch statistics of its output (when the BN normalises with them), and the fused
-    BN consumes them -- the activation is written once and read once. Else run_conv + bn_act."""
-    if isinstance(conv, nn.Conv2d) and isinstance(bn, nn.BatchNorm2d) and conv_fusable(conv, x):
-        use_batch = bn.training or bn.running_mean is None or bn.running_var is None
-        if use_batch:
-            y, part = conv2d(conv, x, stats=True)
-            if fusable(y, bn, residual):
-                return batchnorm_act(y, bn, relu, residual, partials=part)
-            return bn_act(bn, y, relu, residual)
-        return bn_act(bn, conv2d(conv, x), relu, residual)
+    BN consumes them -- the activation is written once and read once. Else run_conv + bn_act.
+    x may be a DeferredBN (its BN runs inside this convolution). With `consumer` (the convolution
+    that reads the result) and no residual, the result may come back as a DeferredBN when that
+    convolution can apply the BN itself (conv_input_bn); pass it on to conv_bn_act."""
+    kw = {}
+    if isinstance(x, DeferredBN):
+        if isinstance(conv, nn.Conv2d) and conv_fusable(conv, x.y) and conv_input_bn(conv, x.y):
+            kw = {"in_ab": x.ab, "in_relu": x.relu}
+            x = x.y
+        else:
+            x = x.materialise()
+    if isinstance(conv, nn.Conv2d) and conv_fusable(conv, x):
+        if isinstance(bn, nn.BatchNorm2d) and _use_batch(bn):
+            y, part = conv2d(conv, x, stats=True, **kw)
+            if not fusable(y, bn, residual):
+                return bn_act(bn, y, relu, residual)
+        else:
+            y, part = conv2d(conv, x, **kw), None
+            if not (isinstance(bn, nn.BatchNorm2d) and fusable(y, bn, residual)):
+                return bn_act(bn, y, relu, residual)
+        if residual is None and isinstance(consumer, nn.Conv2d) and conv_fusable(consumer, y) \
+                and conv_input_bn(consumer, y):
+            return DeferredBN(y, batchnorm_coefficients(y, bn, part), relu, bn, part)
+        return batchnorm_act(y, bn, relu, residual, partials=part)
     return bn_act(bn, run_conv(conv, x), relu, residual)

@@ -15,8 +15,10 @@ convolution + statistics + BN/ReLU/pool call on the GPU) and every
 `relu?(bn(conv(x)) [+ identity])` of the blocks goes through `features.conv_bn_act`: on the GPU
 with channels-last bf16 activations that is the MFMA implicit-GEMM convolution (which also emits
 the BN batch statistics of its output) and one fused HIP BatchNorm(+add)(+ReLU)
-(include/mcgmil_features.h);
-elsewhere (CPU, autograd, fp32) they are the torch layers.
+(include/mcgmil_features.h). A block's first `relu(bn1(.))` is not materialised where the next
+convolution is a 3x3 / stride 1 halo kernel: that convolution applies it to its input patch
+(features.DeferredBN, mcgmil_conv_args.in_ab). Elsewhere (CPU, autograd, fp32) they are the
+torch layers.
 """
 import warnings
 
@@ -68,7 +70,7 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         idt = _identity(self.downsample, x)
-        y = conv_bn_act(self.conv1, self.bn1, x, True)
+        y = conv_bn_act(self.conv1, self.bn1, x, True, consumer=self.conv2)   # maybe deferred
         return conv_bn_act(self.conv2, self.bn2, y, True, idt)
 
 
@@ -88,8 +90,8 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         idt = _identity(self.downsample, x)
-        y = conv_bn_act(self.conv1, self.bn1, x, True)
-        y = conv_bn_act(self.conv2, self.bn2, y, True)
+        y = conv_bn_act(self.conv1, self.bn1, x, True, consumer=self.conv2)   # maybe deferred
+        y = conv_bn_act(self.conv2, self.bn2, y, True, consumer=self.conv3)
         return conv_bn_act(self.conv3, self.bn3, y, True, idt)
 
 

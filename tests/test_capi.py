@@ -189,3 +189,26 @@ def test_conv_stats_parts_and_validation(hip_lib):
     assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 64, 3, 0, 1)), ctypes.byref(p)) == -1
     assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 64, 3, 1, 1, 20000)), ctypes.byref(p)) == -2
     assert hip_lib.mcgmil_conv2d(ctypes.byref(conv(64, 64, 3, 1, 1)), None) == -1   # NULL x / w / y
+    # input BatchNorm: the 3x3 / stride 1 halo kernels only
+    for args, want in ((conv(64, 64, 3, 1, 1, 56), 1), (conv(128, 128, 3, 1, 1, 28), 1),
+                       (conv(64, 128, 3, 2, 1, 56), 0), (conv(64, 128, 1, 1, 0), 0),
+                       (conv(256, 256, 3, 1, 1, 14), 0), (conv(128, 128, 3, 1, 1, 100), 0)):
+        assert hip_lib.mcgmil_conv_input_bn(ctypes.byref(args), ctypes.byref(p)) == 0
+        assert p.value == want, (args.in_channels, args.width, p.value)
+    assert hip_lib.mcgmil_conv_input_bn(ctypes.byref(conv(64, 64, 3, 1, 1, in_relu=2)), ctypes.byref(p)) == -1
+
+
+def test_batchnorm_coefficients_validation(hip_lib):
+    """mcgmil_batchnorm_coefficients argument checks (no launches)."""
+    from mcgmil import _lib
+    ab = ctypes.cast((ctypes.c_float * 128)(), ctypes.c_void_p)
+    a = _lib.BnArgs()
+    a.rows, a.channels, a.dtype = 100, 64, _lib.MCGMIL_BF16
+    assert hip_lib.mcgmil_batchnorm_coefficients(None, ab, None) == -1
+    assert hip_lib.mcgmil_batchnorm_coefficients(ctypes.byref(a), None, None) == -1
+    # batch statistics from a pass over x: x and a workspace are required
+    assert hip_lib.mcgmil_batchnorm_coefficients(ctypes.byref(a), ab, None) == -1
+    a.x = ctypes.c_void_p(4096)
+    assert hip_lib.mcgmil_batchnorm_coefficients(ctypes.byref(a), ab, None) == -4
+    a.channels = 12
+    assert hip_lib.mcgmil_batchnorm_coefficients(ctypes.byref(a), ab, None) == -2

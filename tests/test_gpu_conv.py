@@ -196,3 +196,89 @@ def test_conv_statistics_deterministic(cuda):
         y2, p2 = conv2d(conv, x, stats=True)
         y3 = conv2d(conv, x)
     assert torch.equal(y1, y2) and torch.equal(p1, p2) and torch.equal(y1, y3)
+
+
+# conv(relu?(bn(x))) with the BatchNorm applied to the convolution's input patch (in_ab): both
+# halo kernels (64 -> 64 weights in registers; Cin >= 128 streamed weights, 2-3 channel chunks),
+# tiles spanning several images, odd widths, ragged pixel counts, and an input offset
+INBN_SHAPES = [
+    (3, 64, 56, 56, 64),
+    (9, 64, 8, 6, 64),
+    (3, 64, 30, 17, 64),
+    (2, 64, 20, 60, 64),
+    (4, 128, 25, 20, 128),
+    (2, 192, 17, 30, 256),
+    (3, 128, 28, 28, 128),
+]
+
+
+@pytest.mark.parametrize("shape", INBN_SHAPES)
+@pytest.mark.parametrize("relu", [True, False])
+def test_conv_input_bn_bitwise_equals_unfused(cuda, shape, relu):
+    """conv2d(conv, x, in_ab=ab) is bit-identical to conv2d(conv, batchnorm_act(x, bn)): the
+    kernel rewrites its LDS patch with the apply pass's own arithmetic, padding left at zero.
+    Its BatchNorm statistics of the output match too."""
+    from mcgmil.features import batchnorm_act, batchnorm_coefficients, conv2d, conv_input_bn
+    N, Cin, H, W, Cout = shape
+    conv = _layer(Cin, Cout, 3, 1, 1, cuda, Cin + 2 * Cout)
+    bn = _bn64(Cin, cuda, Cin + 5)
+    g = torch.Generator(device=cuda).manual_seed(N * H + W + Cin)
+    x = (torch.randn(N, Cin, H, W, device=cuda, generator=g) * 2.0 + 0.5).bfloat16()
+    x = x.contiguous(memory_format=torch.channels_last)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        assert conv_input_bn(conv, x)
+        ab = batchnorm_coefficients(x, bn)
+        h = batchnorm_act(x, bn, relu)
+        y_ref, p_ref = conv2d(conv, h, stats=True)
+        y, p = conv2d(conv, x, stats=True, in_ab=ab, in_relu=relu)
+    assert torch.equal(y, y_ref)
+    assert torch.equal(p, p_ref)
+    # and the coefficients are the ones the apply pass used: a, b from the fp64 statistics of x
+    xd = x.double()
+    mean, var = xd.mean(dim=(0, 2, 3)), xd.var(dim=(0, 2, 3), unbiased=False)
+    a = bn.weight.double() / torch.sqrt(var + bn.eps)
+    assert torch.allclose(ab[0].double(), a, rtol=1e-5, atol=0)
+    assert torch.allclose(ab[1].double(), bn.bias.double() - mean * a, rtol=1e-5, atol=1e-5)
+
+
+def test_conv_input_bn_support_and_errors(cuda):
+    """Only the 3x3 / stride 1 halo kernels take in_ab; elsewhere conv2d refuses it."""
+    from mcgmil.features import conv2d, conv_input_bn
+    x = torch.randn(2, 64, 28, 28, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        assert conv_input_bn(_layer(64, 64, 3, 1, 1, cuda, 1), x)
+        assert not conv_input_bn(_layer(64, 128, 3, 2, 1, cuda, 1), x)        # stride 2
+        assert not conv_input_bn(_layer(64, 128, 1, 1, 0, cuda, 1), x)        # 1 x 1
+        x3 = torch.randn(2, 256, 14, 14, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+        assert not conv_input_bn(_layer(256, 256, 3, 1, 1, cuda, 1), x3)      # 14 x 14: 256 x 256 tiles
+        # width 62: the two patches fill the 160-KB LDS, no room for the a, b table
+        x62 = torch.randn(2, 64, 20, 62, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+        assert not conv_input_bn(_layer(64, 64, 3, 1, 1, cuda, 1), x62)
+        ab = torch.zeros(2, 64, device=cuda)
+        with pytest.raises(RuntimeError):
+            conv2d(_layer(64, 128, 3, 2, 1, cuda, 1), x, in_ab=ab)
+        with pytest.raises(ValueError):
+            conv2d(_layer(64, 64, 3, 1, 1, cuda, 1), x, in_ab=torch.zeros(2, 32, device=cuda))
+
+
+def test_backbone_input_bn_bitwise(cuda):
+    """ResNet-18 with its blocks' first BN deferred into the halo convolutions gives bit-identical
+    features to the materialised form (MCGMIL_FUSE_INPUT_BN=0)."""
+    import os
+    from mcgmil.resnet import build_backbone, deactivate_batchnorm, Identity
+    torch.manual_seed(0)
+    net = build_backbone("r18", pretrained=False)
+    net.fc = Identity()
+    net.apply(deactivate_batchnorm)
+    net = net.to(cuda).eval().to(memory_format=torch.channels_last)
+    g = torch.Generator(device=cuda).manual_seed(9)
+    x = torch.rand(10, 3, 112, 112, device=cuda, generator=g).contiguous(memory_format=torch.channels_last)
+    out = {}
+    for flag in ("1", "0"):
+        os.environ["MCGMIL_FUSE_INPUT_BN"] = flag
+        try:
+            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+                out[flag] = net(x).float()
+        finally:
+            os.environ.pop("MCGMIL_FUSE_INPUT_BN", None)
+    assert torch.equal(out["1"], out["0"])
