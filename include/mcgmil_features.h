@@ -74,6 +74,11 @@ typedef struct mcgmil_bn_args {
     const float* partials;      /* optional [num_partials][3][C] (count, mean, M2) blocks of x, as
                                    mcgmil_conv2d's stats: batch statistics from them (Chan's
                                    combination in fp64, fixed order) instead of a pass over x */
+    const float* residual_ab;   /* optional [2][C] (a_c, b_c) of the residual's own BatchNorm (as
+                                   mcgmil_batchnorm_coefficients writes them): the added residual
+                                   is dtype(fmaf(r, a_c, b_c)) -- bit-identical to normalising the
+                                   residual in a pass of its own first (the ResNet downsample
+                                   branch). Needs residual. NULL: r as is */
 } mcgmil_bn_args;
 
 size_t mcgmil_bn_args_size(void);   /* sizeof(mcgmil_bn_args), for binding checks */

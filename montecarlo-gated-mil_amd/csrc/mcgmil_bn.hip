@@ -243,25 +243,32 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_chan_kernel(const float*
 
 // Grid-stride over 8-channel vectors; the total thread count is a multiple of C/8, so every
 // thread keeps one channel group. Two vectors in flight per iteration.
-template <typename E, bool RELU, bool RES>
+// RESBN: the residual gets its own BatchNorm first, rounded to E as a separate pass would store it
+template <typename E, bool RELU, bool RES, bool RESBN = false>
 __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const E* x, const E* res, E* y, long long nvec,
-                                                            int C, const float* __restrict__ ab) {
+                                                            int C, const float* __restrict__ ab,
+                                                            const float* __restrict__ rab = nullptr) {
     const int CG = C >> 3;
     const long long stride = (long long)gridDim.x * kThreads;
     const long long i0 = (long long)blockIdx.x * kThreads + threadIdx.x;
     const int cg = (int)(i0 % CG);
-    float a[8], b[8];
+    float a[8], b[8], ra[8], rb[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         a[j] = ab[cg * 8 + j];
         b[j] = ab[C + cg * 8 + j];
+        if (RESBN) {
+            ra[j] = rab[cg * 8 + j];
+            rb[j] = rab[C + cg * 8 + j];
+        }
     }
     auto one = [&](long long i, const float (&v)[8], const float (&r)[8]) {
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             float t = fmaf(v[j], a[j], b[j]);
-            if (RES) t += r[j];
+            if (RESBN) t += (float)(E)fmaf(r[j], ra[j], rb[j]);
+            else if (RES) t += r[j];
             o[j] = RELU ? fmaxf(t, 0.f) : t;
         }
         store8s(y + i * 8, o);
@@ -370,6 +377,8 @@ int validate(const mcgmil_bn_args* a) {
     if (a->relu != 0 && a->relu != 1) return fail(MCGMIL_E_INVALID, "relu must be 0 or 1");
     if (a->partials && (a->num_partials < 1 || ((uintptr_t)a->partials & 3)))
         return fail(MCGMIL_E_INVALID, "partials need num_partials >= 1 and 4-byte alignment");
+    if (a->residual_ab && (!a->residual || ((uintptr_t)a->residual_ab & 3)))
+        return fail(MCGMIL_E_INVALID, "residual_ab needs a residual and 4-byte alignment");
     if (a->pool_kernel < 0) return fail(MCGMIL_E_INVALID, "pool_kernel must be >= 0");
     if (a->pool_kernel > 0) {
         if (a->batch < 1 || a->height < 1 || a->width < 1 ||
@@ -385,7 +394,7 @@ int validate(const mcgmil_bn_args* a) {
     return MCGMIL_OK;
 }
 
-template <typename E, bool RELU, bool RES>
+template <typename E, bool RELU, bool RES, bool RESBN = false>
 void launch_apply(const mcgmil_bn_args* a, const float* ab, hipStream_t s) {
     const long long nvec = a->rows * (a->channels / 8);
     const int CG = a->channels / 8;
@@ -394,9 +403,9 @@ void launch_apply(const mcgmil_bn_args* a, const float* ab, hipStream_t s) {
     long long want = (nvec + 2LL * kThreads - 1) / (2LL * kThreads);
     if (want > 4096) want = 4096;
     long long blocks = (want + unit - 1) / unit * unit;
-    hipLaunchKernelGGL((bn_apply_kernel<E, RELU, RES>), dim3((unsigned)blocks), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL((bn_apply_kernel<E, RELU, RES, RESBN>), dim3((unsigned)blocks), dim3(kThreads), 0, s,
                        static_cast<const E*>(a->x), static_cast<const E*>(a->residual),
-                       static_cast<E*>(a->y), nvec, a->channels, ab);
+                       static_cast<E*>(a->y), nvec, a->channels, ab, a->residual_ab);
 }
 
 // finalize (statistics from `parts` partial sums around the per-channel shift row `shift`, or
@@ -420,7 +429,10 @@ int apply_step(const mcgmil_bn_args* a, const float* ab, hipStream_t s) {
         return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "batchnorm pool launch");
     }
     const bool res = a->residual != nullptr;
-    if (a->relu) {
+    if (res && a->residual_ab) {
+        if (a->relu) launch_apply<E, true, true, true>(a, ab, s);
+        else launch_apply<E, false, true, true>(a, ab, s);
+    } else if (a->relu) {
         if (res) launch_apply<E, true, true>(a, ab, s);
         else launch_apply<E, true, false>(a, ab, s);
     } else {
@@ -521,6 +533,7 @@ int mcgmil_batchnorm_coefficients(const mcgmil_bn_args* a, float* ab, void* stre
     // the apply-side fields do not matter here: validate the rest as mcgmil_batchnorm_act would
     mcgmil_bn_args b = *a;
     b.residual = nullptr;
+    b.residual_ab = nullptr;
     b.pool_kernel = 0;
     b.relu = 0;
     // x is only read by the statistics pass; y never (a placeholder keeps validate() generic)

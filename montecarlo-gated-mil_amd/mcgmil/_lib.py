@@ -111,6 +111,7 @@ class BnArgs(ctypes.Structure):
         ("pool_pad", ctypes.c_int32), ("num_partials", ctypes.c_int32),
         ("batch_mean", _vp), ("batch_invstd", _vp),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t), ("partials", _vp),
+        ("residual_ab", _vp),
     ]
 
 

@@ -124,10 +124,15 @@ def packed_conv_weight(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     return packed
 
 
+def fold_enabled() -> bool:
+    """MCGMIL_FUSE_INPUT_BN=0 materialises every BatchNorm output (no DeferredBN)."""
+    return os.environ.get("MCGMIL_FUSE_INPUT_BN", "1") != "0"
+
+
 def conv_input_bn(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     """Whether conv2d(conv, x, in_ab=...) can apply an input BatchNorm inside the convolution
-    (mcgmil_conv_input_bn: the 3x3 / stride 1 halo kernels). MCGMIL_FUSE_INPUT_BN=0 disables it."""
-    if os.environ.get("MCGMIL_FUSE_INPUT_BN", "1") == "0":
+    (mcgmil_conv_input_bn: the 3x3 / stride 1 halo kernels); False with MCGMIL_FUSE_INPUT_BN=0."""
+    if not fold_enabled():
         return False
     L = _lib.load()
     ok = ctypes.c_int32()
@@ -201,11 +206,13 @@ def _pool_params(pool) -> Optional[tuple]:
 def batchnorm_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool,
                   residual: Optional[torch.Tensor] = None,
                   pool: Optional[nn.MaxPool2d] = None,
-                  partials: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  partials: Optional[torch.Tensor] = None,
+                  residual_ab: Optional[torch.Tensor] = None) -> torch.Tensor:
     """relu?(bn(x) [+ residual]) for a channels-last [N, C, H, W] activation (see fusable), or
     pool(relu?(bn(x))) with a fusable max-pool (the ResNet stem) without materialising the
     activation. `partials` ([parts, 3, C] from conv2d(..., stats=True)) supplies the batch
-    statistics of x, so x is read once."""
+    statistics of x, so x is read once. `residual_ab` ([2, C] from batchnorm_coefficients) is the
+    residual's own BatchNorm, applied on the fly (bit-identical to normalising it first)."""
     if not fusable(x, bn, residual):
         raise ValueError("batchnorm_act needs a CUDA channels-last bf16/fp32 activation with "
                          "C % 8 == 0, C <= 2048 and no autograd (see mcgmil.features.fusable)")
@@ -237,6 +244,11 @@ def batchnorm_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool,
     a.x, a.y, a.residual = p(x), p(y), p(residual)
     a.gamma, a.beta, a.running_mean, a.running_var = p(gamma), p(beta), p(rmean), p(rvar)
     a.eps, a.relu = float(bn.eps), int(bool(relu))
+    if residual_ab is not None:
+        if residual is None or residual_ab.shape != (2, C) or residual_ab.dtype != torch.float32 or \
+                residual_ab.device != dev or not residual_ab.is_contiguous():
+            raise ValueError("residual_ab needs a residual and a contiguous fp32 [2, C] tensor on x's device")
+        a.residual_ab = p(residual_ab)
     if partials is not None and use_batch:
         if partials.dim() != 3 or partials.shape[1:] != (3, C) or not partials.is_contiguous() or \
                 partials.dtype != torch.float32 or partials.device != dev:
@@ -440,14 +452,22 @@ def _use_batch(bn: nn.BatchNorm2d) -> bool:
     return bn.training or bn.running_mean is None or bn.running_var is None
 
 
-def conv_bn_act(conv: nn.Module, bn: nn.Module, x, relu: bool,
-                residual: Optional[torch.Tensor] = None, consumer: Optional[nn.Module] = None):
+def conv_bn_act(conv: nn.Module, bn: nn.Module, x, relu: bool, residual=None,
+                consumer: Optional[nn.Module] = None, as_residual: bool = False):
     """The blocks' `relu?(bn(conv(x)) [+ residual])`: on the GPU the MFMA convolution also emits
     the BatchNorm batch statistics of its output (when the BN normalises with them), and the fused
     BN consumes them -- the activation is written once and read once. Else run_conv + bn_act.
     x may be a DeferredBN (its BN runs inside this convolution). With `consumer` (the convolution
     that reads the result) and no residual, the result may come back as a DeferredBN when that
-    convolution can apply the BN itself (conv_input_bn); pass it on to conv_bn_act."""
+    convolution can apply the BN itself (conv_input_bn); pass it on to conv_bn_act. With
+    as_residual (the downsample branch) a ReLU-free result may come back as a DeferredBN too; pass
+    it as conv_bn_act's residual, whose fused BN applies it while adding."""
+    res_ab, res_deferred = None, None
+    if isinstance(residual, DeferredBN):
+        if residual.relu:
+            residual = residual.materialise()
+        else:
+            res_deferred, residual, res_ab = residual, residual.y, residual.ab
     kw = {}
     if isinstance(x, DeferredBN):
         if isinstance(conv, nn.Conv2d) and conv_fusable(conv, x.y) and conv_input_bn(conv, x.y):
@@ -458,14 +478,12 @@ def conv_bn_act(conv: nn.Module, bn: nn.Module, x, relu: bool,
     if isinstance(conv, nn.Conv2d) and conv_fusable(conv, x):
         if isinstance(bn, nn.BatchNorm2d) and _use_batch(bn):
             y, part = conv2d(conv, x, stats=True, **kw)
-            if not fusable(y, bn, residual):
-                return bn_act(bn, y, relu, residual)
         else:
             y, part = conv2d(conv, x, **kw), None
-            if not (isinstance(bn, nn.BatchNorm2d) and fusable(y, bn, residual)):
-                return bn_act(bn, y, relu, residual)
-        if residual is None and isinstance(consumer, nn.Conv2d) and conv_fusable(consumer, y) \
-                and conv_input_bn(consumer, y):
+        if not (isinstance(bn, nn.BatchNorm2d) and fusable(y, bn, residual)):
+            return bn_act(bn, y, relu, res_deferred.materialise() if res_deferred else residual)
+        if residual is None and ((isinstance(consumer, nn.Conv2d) and conv_fusable(consumer, y)
+                                  and conv_input_bn(consumer, y)) or (as_residual and not relu and fold_enabled())):
             return DeferredBN(y, batchnorm_coefficients(y, bn, part), relu, bn, part)
-        return batchnorm_act(y, bn, relu, residual, partials=part)
-    return bn_act(bn, run_conv(conv, x), relu, residual)
+        return batchnorm_act(y, bn, relu, residual, partials=part, residual_ab=res_ab)
+    return bn_act(bn, run_conv(conv, x), relu, res_deferred.materialise() if res_deferred else residual)

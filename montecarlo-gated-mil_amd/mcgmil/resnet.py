@@ -48,7 +48,7 @@ def _identity(down, x):
     if down is None:
         return x
     if isinstance(down, nn.Sequential) and len(down) == 2 and isinstance(down[1], nn.BatchNorm2d):
-        return conv_bn_act(down[0], down[1], x, False)
+        return conv_bn_act(down[0], down[1], x, False, as_residual=True)   # maybe deferred
     return down(x)
 
 

@@ -282,3 +282,21 @@ def test_backbone_input_bn_bitwise(cuda):
         finally:
             os.environ.pop("MCGMIL_FUSE_INPUT_BN", None)
     assert torch.equal(out["1"], out["0"])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_residual_bn_bitwise_equals_unfused(cuda, dtype):
+    """batchnorm_act(y, bn2, relu, residual=r, residual_ab=ab_d) equals normalising r in a pass of
+    its own first (the downsample branch), bit for bit."""
+    from mcgmil.features import batchnorm_act, batchnorm_coefficients
+    bn2, bnd = _bn64(128, cuda, 11), _bn64(128, cuda, 12)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    y = (torch.randn(5, 128, 14, 13, device=cuda, generator=g) * 3 + 1).to(dtype).contiguous(
+        memory_format=torch.channels_last)
+    r = (torch.randn(5, 128, 14, 13, device=cuda, generator=g) * 2 - 1).to(dtype).contiguous(
+        memory_format=torch.channels_last)
+    with torch.no_grad():
+        ab_d = batchnorm_coefficients(r, bnd)
+        ref = batchnorm_act(y, bn2, True, residual=batchnorm_act(r, bnd, False))
+        out = batchnorm_act(y, bn2, True, residual=r, residual_ab=ab_d)
+    assert torch.equal(out, ref)
