@@ -341,6 +341,53 @@ __global__ __launch_bounds__(kThreads) void bn_pool_kernel(const E* __restrict__
     }
 }
 
+// The stem's pooling pass after its convolution took the horizontal half (mcgmil_stem.hip, HP):
+// x is [N, H, W / 2, C] of row maxima, stored negated where a_c < 0 (sign of a = sign of gamma).
+// Thread per (output pixel, 8-channel group): the vertical 3-row window (stride 2, pad 1), the
+// sign restored, then the BN + ReLU -- equal to bn_pool_kernel's max over the 3 x 3 window of
+// fmaf(v, a, b) because fmaf is monotonic in v (non-increasing where a_c < 0).
+template <bool RELU>
+__global__ __launch_bounds__(kThreads) void bn_vpool_kernel(const __bf16* __restrict__ x, __bf16* __restrict__ y,
+                                                            int H, int Wp, int Ho, long long nvec, int C,
+                                                            const float* __restrict__ ab) {
+    const int CG = C >> 3;
+    const long long stride = (long long)gridDim.x * kThreads;
+    const long long i0 = (long long)blockIdx.x * kThreads + threadIdx.x;
+    const int cg = (int)(i0 % CG);
+    float a[8], b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        a[j] = ab[cg * 8 + j];
+        b[j] = ab[C + cg * 8 + j];
+    }
+    for (long long i = i0; i < nvec; i += stride) {
+        const long long pix = i / CG;
+        const int pw = (int)(pix % Wp);
+        const long long t = pix / Wp;
+        const int oh = (int)(t % Ho);
+        const long long n = t / Ho;
+        float m[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+        for (int kh = 0; kh < 3; ++kh) {
+            const int ih = 2 * oh - 1 + kh;
+            if (ih < 0 || ih >= H) continue;
+            float v[8];
+            load8(x + (((n * H + ih) * (long long)Wp + pw) * C + cg * 8), v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], v[j]);
+        }
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float v = signbit(a[j]) ? -m[j] : m[j];
+            const float r = fmaf(v, a[j], b[j]);
+            o[j] = RELU ? fmaxf(r, 0.f) : r;
+        }
+        store8s(y + i * 8, o);
+    }
+}
+
 int pooled_dim(int size, const mcgmil_bn_args* a) {
     return (size + 2 * a->pool_pad - a->pool_kernel) / a->pool_stride + 1;
 }
@@ -412,8 +459,21 @@ void launch_apply(const mcgmil_bn_args* a, const float* ab, hipStream_t s) {
 // the running statistics) then the normalise / pool pass; ab lives at the workspace start
 // the normalise / pool pass with a, b at ab
 template <typename E>
-int apply_step(const mcgmil_bn_args* a, const float* ab, hipStream_t s) {
+int apply_step(const mcgmil_bn_args* a, const float* ab, hipStream_t s, bool hpooled = false) {
     const int C = a->channels;
+    if (hpooled) {      // bf16 only (the stem); a describes the unpooled [N, H, W, C] activation
+        const int Ho = pooled_dim(a->height, a), Wp = a->width / 2;
+        const long long nvec = (long long)a->batch * Ho * Wp * (C / 8);
+        const int unit = (C / 8) / std::gcd(C / 8, kThreads);
+        long long want = (nvec + kThreads - 1) / kThreads;
+        if (want > 8192) want = 8192;
+        const long long blocks = (want + unit - 1) / unit * unit;
+        auto k = a->relu ? bn_vpool_kernel<true> : bn_vpool_kernel<false>;
+        hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kThreads), 0, s, static_cast<const __bf16*>(a->x),
+                           static_cast<__bf16*>(a->y), a->height, Wp, Ho, nvec, C, ab);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "batchnorm vertical pool launch");
+    }
     if (a->pool_kernel > 0) {
         const int Ho = pooled_dim(a->height, a), Wo = pooled_dim(a->width, a);
         const long long nvec = (long long)a->batch * Ho * Wo * (C / 8);
@@ -449,7 +509,7 @@ int apply_step(const mcgmil_bn_args* a, const float* ab, hipStream_t s) {
 // start, then the apply / pool pass
 template <typename E>
 int finish(const mcgmil_bn_args* a, const float* part, int parts, const E* shift, hipStream_t s,
-           float* ab_out = nullptr) {
+           float* ab_out = nullptr, bool hpooled = false) {
     const int C = a->channels;
     float* ab = ab_out ? ab_out : static_cast<float*>(a->workspace);   // [2][C]
     hipLaunchKernelGGL(bn_finalize_kernel<E>, dim3((C + kFinCh - 1) / kFinCh), dim3(kThreads), 0, s, part, parts, a->rows,
@@ -459,7 +519,7 @@ int finish(const mcgmil_bn_args* a, const float* part, int parts, const E* shift
         const hipError_t e = hipGetLastError();
         return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "batchnorm finalize launch");
     }
-    return apply_step<E>(a, ab, s);
+    return apply_step<E>(a, ab, s, hpooled);
 }
 
 template <typename E>
@@ -495,14 +555,16 @@ namespace mcgmil_detail {
 // partial sums itself (the stem convolution's epilogue): `parts` blocks of [2][C] fp32 sums of
 // (x - shift_c) and (x - shift_c)^2, shift_row the bf16 [C] shift. a->workspace needs 2 * C floats.
 int bn_finish_bf16(const mcgmil_bn_args* a, const float* part, int parts, const void* shift_row,
-                   hipStream_t s) {
+                   hipStream_t s, bool hpooled) {
     if (int rc = validate(a)) return rc;
     if (a->dtype != MCGMIL_BF16) return fail(MCGMIL_E_INVALID, "bn_finish_bf16 needs bf16");
     if (!a->workspace || a->workspace_bytes < 2 * (size_t)a->channels * sizeof(float))
         return fail(MCGMIL_E_WORKSPACE, "bn_finish_bf16: workspace smaller than 2 * C floats");
     if (!a->running_mean && (parts < 1 || !part || !shift_row))
         return fail(MCGMIL_E_INVALID, "bn_finish_bf16: batch statistics need partials and a shift");
-    return finish<__bf16>(a, part, parts, static_cast<const __bf16*>(shift_row), s);
+    if (hpooled && (a->pool_kernel != 3 || a->pool_stride != 2 || a->pool_pad != 1 || (a->width & 1)))
+        return fail(MCGMIL_E_INVALID, "bn_finish_bf16: the row-pooled input needs a 3 x 3 / 2 / pad 1 pool, even width");
+    return finish<__bf16>(a, part, parts, static_cast<const __bf16*>(shift_row), s, nullptr, hpooled);
 }
 
 }  // namespace mcgmil_detail

@@ -26,6 +26,9 @@
 // and read once.
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+#include <string.h>
+
 #include <atomic>
 #include <string>
 
@@ -35,7 +38,7 @@
 
 namespace mcgmil_detail {
 int bn_finish_bf16(const mcgmil_bn_args* a, const float* part, int parts, const void* shift_row,
-                   hipStream_t s);
+                   hipStream_t s, bool hpooled);
 }
 
 namespace {
@@ -57,6 +60,7 @@ struct StemGeom {
     const __bf16* shift;
     const uint32_t* zero;   // 64 zero dwords (padding source of the LDS-DMA staging)
     float* part;
+    const float* gamma;     // HP: the BN weight (its signs), or NULL
     int N, Cin, H, W, OH, OW, k, pad, P;
     int RR;          // staged rows per channel: 2 (kTH - 1) + k
     int pitch;       // LDS dwords per staged row
@@ -100,7 +104,7 @@ int geometry(const mcgmil_stem_args* a, Geometry* out) {
     g.pitch = (g.wd + 63) / 64 * 64 + 16;   // whole 64-dword DMA pieces, 16 (mod 64)
     g.plane = g.RR * g.pitch;
     while ((g.plane - g.k * g.pitch) % 64 != 0) ++g.plane;
-    G.lds = (size_t)2 * g.Cin * g.plane * 4 + (size_t)kTH * 16 * kCout * 2;   // + epilogue scratch
+    G.lds = (size_t)2 * g.Cin * g.plane * 4 + (size_t)kTH * 17 * kCout * 2;   // + epilogue scratch, carry
     if (G.lds > (size_t)kLdsBytes) return fail(MCGMIL_E_UNSUPPORTED, "stem tile exceeds 64 KiB of LDS");
     g.TPI = (OH + kTH - 1) / kTH;
     const long long tiles = (long long)g.N * g.TPI;
@@ -172,7 +176,13 @@ __global__ __launch_bounds__(256) void stem_prep_kernel(const StemGeom g, int KS
     (void)KS;
 }
 
-template <int KS, bool STATS>
+// HP (the ResNet 3x3 / 2 / pad 1 max-pool, OW even): the epilogue also takes the horizontal
+// 3-wide, stride-2 maximum of each row and stores only that, [N, OH, OW / 2, 64] -- half the
+// activation bytes written here and read by the pooling pass (bn_vpool_kernel), which takes the
+// vertical maximum. Max-pooling commutes with the BN only channel by channel: where a_c < 0 (the
+// sign of gamma_c) the pool of BN(x) is BN of the MINIMUM, so those channels are stored negated
+// (bf16 negation is exact) and their maximum is the negated minimum.
+template <int KS, bool STATS, bool HP>
 __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, p = lane & 15;
@@ -236,6 +246,17 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
 
     const int FR = (g.OW + 15) >> 4;
     __bf16* scratch = reinterpret_cast<__bf16*>(lds + 2 * buf_dw) + wave * 16 * kCout;   // 2 KiB per wave
+    // HP: lane = (pooled pixel j of the fragment, 8-channel chunk hc); the chunk's sign flips
+    __bf16* carry = reinterpret_cast<__bf16*>(lds + 2 * buf_dw) + kTH * 16 * kCout + wave * kCout;
+    const int hj = lane >> 3, hc = lane & 7;
+    uint32_t hflip[4] = {0u, 0u, 0u, 0u};
+    if (HP && g.gamma) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+            hflip[d] = (__float_as_uint(g.gamma[8 * hc + 2 * d]) >> 31 << 15) |
+                       (__float_as_uint(g.gamma[8 * hc + 2 * d + 1]) >> 31 << 31);
+    }
+    const int PW = g.OW >> 1;
     if (t0 < t1) stage(t0, 0);
     __syncthreads();
     for (int t = t0; t < t1; ++t) {
@@ -284,12 +305,47 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
                 }
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
+                if (HP) {
+                    // pooled pixel 8 f + hj = max over fragment pixels 2 hj - 1 (the carry from the
+                    // previous fragment when hj = 0; padding when f = 0), 2 hj, 2 hj + 1
+                    auto px = [&](int pp) {
+                        uint4 u = __builtin_bit_cast(uint4, *reinterpret_cast<const bf16x8*>(
+                                                                 scratch + pp * 64 + ((hc ^ (pp & 7)) << 3)));
+                        u.x ^= hflip[0]; u.y ^= hflip[1]; u.z ^= hflip[2]; u.w ^= hflip[3];
+                        return u;
+                    };
+                    const uint4 u0 = px(2 * hj), u1 = px(2 * hj + 1);
+                    uint4 um = u0;
+                    bool three = hj > 0 || f > 0;
+                    if (hj > 0) um = px(2 * hj - 1);
+                    else if (f > 0) um = *reinterpret_cast<const uint4*>(carry + 8 * hc);
+                    const uint32_t w0[4] = {u0.x, u0.y, u0.z, u0.w}, w1[4] = {u1.x, u1.y, u1.z, u1.w},
+                                   wm[4] = {um.x, um.y, um.z, um.w};
+                    uint32_t o[4];
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int pp = (lane >> 3) + 8 * h, c = lane & 7;
-                    const bf16x8 v = *reinterpret_cast<const bf16x8*>(scratch + pp * 64 + ((c ^ (pp & 7)) << 3));
-                    if (16 * f + pp < g.OW)
-                        *reinterpret_cast<bf16x8*>(yrow + (size_t)(16 * f + pp) * kCout + 8 * c) = v;
+                    for (int d = 0; d < 4; ++d) {
+                        float lo = fmaxf(__uint_as_float(w0[d] << 16), __uint_as_float(w1[d] << 16));
+                        float hi = fmaxf(__uint_as_float(w0[d] & 0xFFFF0000u), __uint_as_float(w1[d] & 0xFFFF0000u));
+                        if (three) {
+                            lo = fmaxf(lo, __uint_as_float(wm[d] << 16));
+                            hi = fmaxf(hi, __uint_as_float(wm[d] & 0xFFFF0000u));
+                        }
+                        o[d] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xFFFF0000u);   // exact
+                    }
+                    asm volatile("" ::: "memory");
+                    if (hj == 7) *reinterpret_cast<uint4*>(carry + 8 * hc) = u1;   // pixel 15, sign-adjusted
+                    const int pw = 8 * f + hj;
+                    if (pw < PW)
+                        *reinterpret_cast<uint4*>(g.y + (((size_t)n * g.OH + oh) * PW + pw) * kCout + 8 * hc) =
+                            make_uint4(o[0], o[1], o[2], o[3]);
+                } else {
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int pp = (lane >> 3) + 8 * h, c = lane & 7;
+                        const bf16x8 v = *reinterpret_cast<const bf16x8*>(scratch + pp * 64 + ((c ^ (pp & 7)) << 3));
+                        if (16 * f + pp < g.OW)
+                            *reinterpret_cast<bf16x8*>(yrow + (size_t)(16 * f + pp) * kCout + 8 * c) = v;
+                    }
                 }
                 asm volatile("" ::: "memory");
             }
@@ -326,11 +382,10 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
 }
 
 template <int KS>
-void launch_conv(const StemGeom& g, int grid, size_t lds, bool stats, hipStream_t s) {
-    if (stats)
-        hipLaunchKernelGGL((stem_conv_kernel<KS, true>), dim3(grid), dim3(kThreads), lds, s, g);
-    else
-        hipLaunchKernelGGL((stem_conv_kernel<KS, false>), dim3(grid), dim3(kThreads), lds, s, g);
+void launch_conv(const StemGeom& g, int grid, size_t lds, bool stats, bool hp, hipStream_t s) {
+    auto k = stats ? (hp ? stem_conv_kernel<KS, true, true> : stem_conv_kernel<KS, true, false>)
+                   : (hp ? stem_conv_kernel<KS, false, true> : stem_conv_kernel<KS, false, false>);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, s, g);
 }
 
 int cu_count() {
@@ -435,17 +490,22 @@ int mcgmil_stem_forward(const mcgmil_stem_args* a, void* stream) {
     g.shift = reinterpret_cast<const __bf16*>(ws + c.shift);
     g.zero = reinterpret_cast<const uint32_t*>(ws + c.shift + 128);
     g.part = reinterpret_cast<float*>(ws + c.part);
+    g.gamma = a->gamma;
+    // the ResNet pool (3 x 3, stride 2, pad 1) on an even width: horizontal half in the epilogue
+    const char* hp_env = getenv("MCGMIL_STEM_HPOOL");
+    const bool hp = a->pool_kernel == 3 && a->pool_stride == 2 && a->pool_pad == 1 && G.OW % 2 == 0 &&
+                    !(hp_env && !strcmp(hp_env, "0"));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(stem_prep_kernel, dim3(1), dim3(256), 0, s, g, G.KS, (int)stats);
     switch (G.KS) {
-        case 1: launch_conv<1>(g, c.grid, G.lds, stats, s); break;
-        case 2: launch_conv<2>(g, c.grid, G.lds, stats, s); break;
-        case 3: launch_conv<3>(g, c.grid, G.lds, stats, s); break;
-        case 4: launch_conv<4>(g, c.grid, G.lds, stats, s); break;
-        case 5: launch_conv<5>(g, c.grid, G.lds, stats, s); break;
-        case 6: launch_conv<6>(g, c.grid, G.lds, stats, s); break;
-        case 7: launch_conv<7>(g, c.grid, G.lds, stats, s); break;
-        default: launch_conv<8>(g, c.grid, G.lds, stats, s); break;
+        case 1: launch_conv<1>(g, c.grid, G.lds, stats, hp, s); break;
+        case 2: launch_conv<2>(g, c.grid, G.lds, stats, hp, s); break;
+        case 3: launch_conv<3>(g, c.grid, G.lds, stats, hp, s); break;
+        case 4: launch_conv<4>(g, c.grid, G.lds, stats, hp, s); break;
+        case 5: launch_conv<5>(g, c.grid, G.lds, stats, hp, s); break;
+        case 6: launch_conv<6>(g, c.grid, G.lds, stats, hp, s); break;
+        case 7: launch_conv<7>(g, c.grid, G.lds, stats, hp, s); break;
+        default: launch_conv<8>(g, c.grid, G.lds, stats, hp, s); break;
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "stem_conv_kernel launch");
@@ -471,7 +531,7 @@ int mcgmil_stem_forward(const mcgmil_stem_args* a, void* stream) {
     b.batch_invstd = a->batch_invstd;
     b.workspace = ws + c.bn;
     b.workspace_bytes = c.total - c.bn;
-    return mcgmil_detail::bn_finish_bf16(&b, g.part, stats ? c.grid : 0, g.shift, s);
+    return mcgmil_detail::bn_finish_bf16(&b, g.part, stats ? c.grid : 0, g.shift, s, hp);
 }
 
 }  // extern "C"

@@ -152,3 +152,30 @@ def test_stem_fusable_gates(cuda):
         bt = nn.BatchNorm2d(64).to(cuda).train()
         assert not stem_fusable(conv, bt, pool, x)                                 # running-stat update
     assert not stem_fusable(conv, bn, pool, x)                                     # autograd
+
+
+@pytest.mark.parametrize("shape", [(6, 3, 224, 224), (1, 3, 12, 8), (2, 3, 40, 64), (2, 3, 36, 44)])
+@pytest.mark.parametrize("running", [False, True])
+def test_stem_row_pooled_epilogue_bitwise(cuda, shape, running):
+    """The 3 x 3 / 2 pool split into a horizontal half in the convolution epilogue and a vertical
+    pass (negated channels where gamma < 0, zero gammas included) equals the unsplit pooling pass
+    bit for bit (MCGMIL_STEM_HPOOL=0); full and partial 16-pixel fragments."""
+    import os
+    from mcgmil.features import stem
+    N, C, H, W = shape
+    conv, bn = _stem_layers(C, 7, 3, cuda, H + W, running)
+    with torch.no_grad():
+        bn.weight[3] = 0.0
+        bn.weight[11] = -0.0
+    pool = nn.MaxPool2d(3, 2, 1)
+    g = torch.Generator(device=cuda).manual_seed(N + H)
+    x = (torch.randn(N, C, H, W, device=cuda, generator=g) * 1.5).bfloat16()
+    outs = {}
+    for flag in ("1", "0"):
+        os.environ["MCGMIL_STEM_HPOOL"] = flag
+        try:
+            with torch.no_grad():
+                outs[flag] = stem(conv, bn, True, pool, x)
+        finally:
+            os.environ.pop("MCGMIL_STEM_HPOOL", None)
+    assert torch.equal(outs["1"], outs["0"])
