@@ -231,8 +231,10 @@ def test_conv_input_bn_bitwise_equals_unfused(cuda, shape, relu):
         h = batchnorm_act(x, bn, relu)
         y_ref, p_ref = conv2d(conv, h, stats=True)
         y, p = conv2d(conv, x, stats=True, in_ab=ab, in_relu=relu)
+        y_nostats = conv2d(conv, x, in_ab=ab, in_relu=relu)     # the kernel without the statistics
     assert torch.equal(y, y_ref)
     assert torch.equal(p, p_ref)
+    assert torch.equal(y_nostats, y_ref)
     # and the coefficients are the ones the apply pass used: a, b from the fp64 statistics of x
     xd = x.double()
     mean, var = xd.mean(dim=(0, 2, 3)), xd.var(dim=(0, 2, 3), unbiased=False)
@@ -300,3 +302,32 @@ def test_residual_bn_bitwise_equals_unfused(cuda, dtype):
         ref = batchnorm_act(y, bn2, True, residual=batchnorm_act(r, bnd, False))
         out = batchnorm_act(y, bn2, True, residual=r, residual_ab=ab_d)
     assert torch.equal(out, ref)
+
+
+def test_backbone_running_statistics_folds_bitwise(cuda):
+    """With BatchNorms on running statistics (eval without deactivate_batchnorm), the folds use the
+    running coefficients: bit-identical to the materialised form."""
+    import os
+    from mcgmil.resnet import build_backbone, Identity
+    torch.manual_seed(1)
+    net = build_backbone("r18", pretrained=False)
+    net.fc = Identity()
+    with torch.no_grad():
+        for m in net.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 1.5)
+                m.weight[::9] *= -1.0
+    net = net.to(cuda).eval().to(memory_format=torch.channels_last)
+    g = torch.Generator(device=cuda).manual_seed(4)
+    x = torch.rand(6, 3, 112, 112, device=cuda, generator=g).contiguous(memory_format=torch.channels_last)
+    out = {}
+    for flag in ("1", "0"):
+        os.environ["MCGMIL_FUSE_INPUT_BN"] = flag
+        try:
+            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+                out[flag] = net(x).float()
+        finally:
+            os.environ.pop("MCGMIL_FUSE_INPUT_BN", None)
+    assert torch.equal(out["1"], out["0"])
+    assert torch.isfinite(out["1"]).all()
