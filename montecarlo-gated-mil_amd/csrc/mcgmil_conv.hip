@@ -516,8 +516,17 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
         __syncthreads();
     }
 
+    int need_px = hg.patch_px;   // pixels of the in-flight patch that the tile reads
     auto issue = [&](int tile, int buf) {
         const int m0 = tile * kBM;
+        {   // the tile's last output pixel, tap (2, 2), bounds the patch pixels it reads: most tiles
+            // need ~3/4 of the worst-case patch (no image boundary inside the tile)
+            const int n0 = m0 / OHW, oh0 = (m0 - n0 * OHW) / g.OW;
+            const int ml = m0 + kBM - 1 < g.M ? m0 + kBM - 1 : g.M - 1;
+            const int nl = ml / OHW, rl = ml - nl * OHW, ohl = rl / g.OW, owl = rl - ohl * g.OW;
+            const int need = (((nl - n0) * HP + ohl - oh0 + 2) * WP + owl + 3 + 7) & ~7;
+            need_px = need < hg.patch_px ? need : hg.patch_px;
+        }
         int n = m0 / OHW;
         int prel = (m0 - n * OHW) / g.OW + rr0;         // padded row (relative to image n) of p
         int col = col0;
@@ -527,7 +536,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
         }
         unsigned char* Lp = smem + buf * patch_bytes;
         okm = 0;
-        for (int piece = wave, k = 0; piece * 8 < hg.patch_px; piece += 8, ++k) {
+        for (int piece = wave, k = 0; piece * 8 < need_px; piece += 8, ++k) {
             const int p = piece * 8 + (lane >> 3);
             const int c = (lane & 7) ^ ((p >> 1) & 7);     // source chunk of this lane's slot
             const int ih = prel - 1, iw = col - 1;
@@ -564,7 +573,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
             }
             // this wave's pieces wave + 8 k, four per LDS round trip
             const uint32_t base = lds_addr(smem + buf * patch_bytes) + lane * 16 + wave * 1024;
-            const int np = (hg.patch_px / 8 - wave + 7) / 8;
+            const int np = (need_px / 8 - wave + 7) / 8;
             for (int k0 = 0; k0 < np; k0 += 4) {
                 uint32_t ad[4];
 #pragma unroll
