@@ -20,6 +20,11 @@ ARCH = os.environ.get("MCGMIL_OFFLOAD_ARCH", "gfx950")
 # transcendental then sometimes reads the new value (nondeterministic low halves of the gate
 # epilogue, found by scripts/probe_determinism.py). Scalar fp32 VALU is hazard-checked.
 DEVICE_FLAGS = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+# Per-source flags. The MCDO gate kernels are scheduled with LLVM's max-ILP strategy: +3.0% on the
+# bf16 separate-heads kernel and +1.1% shared, -1.8% on fp32 separate heads, measured in one process
+# with scripts/probe_gate.py (MCGMIL_PROBE_LIBS; profiles/r01/probe_sched.log). The convolution
+# and BatchNorm sources keep the default scheduler.
+SOURCE_FLAGS = {"mcgmil.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
 
 
 def _stale(out: str = LIB) -> bool:
@@ -40,12 +45,22 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
         return out
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
     tmp = out + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall",
-           "-Werror", f"-I{INCLUDE}", "-o", tmp] + DEVICE_FLAGS + [f"-D{d}" for d in defines] + \
-          [os.path.join(CSRC, s) for s in SOURCES]
+    objs = []
+    for src in SOURCES:     # one object per source (per-source flags), then one shared library
+        obj = f"{out}.{src}.o"
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-c", "-fPIC", "-Wall", "-Werror",
+               f"-I{INCLUDE}", "-o", obj] + DEVICE_FLAGS + SOURCE_FLAGS.get(src, []) + \
+              [f"-D{d}" for d in defines] + [os.path.join(CSRC, src)]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
+    for obj in objs:
+        os.remove(obj)
     os.replace(tmp, out)
     return out
 
