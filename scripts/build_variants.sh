@@ -16,9 +16,21 @@ for spec in "$@"; do
         git archive "$rev" montecarlo-gated-mil_amd/csrc include | tar -x -C "$tmp"
         src=$tmp/montecarlo-gated-mil_amd/csrc; inc=$tmp/include
     fi
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -I"$inc" \
-        -Xclang -target-feature -Xclang -packed-fp32-ops $defs \
-        -o "$OUT/$name.so" "$src/mcgmil.hip" "$src/mcgmil_image.hip" $(for f in mcgmil_bn.hip mcgmil_conv.hip mcgmil_stem.hip; do [ -f "$src/$f" ] && echo "$src/$f"; done) 2>&1 | grep -v packed-fp32-ops || true &
+    # per source, as mcgmil/_build.py: the gate kernels (mcgmil.hip) with the max-ILP scheduler
+    (
+        objs=""
+        for f in mcgmil.hip mcgmil_image.hip mcgmil_bn.hip mcgmil_conv.hip mcgmil_stem.hip; do
+            [ -f "$src/$f" ] || continue
+            extra=""
+            [ "$f" = mcgmil.hip ] && extra="-mllvm -amdgpu-sched-strategy=max-ilp"
+            /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -c -fPIC -I"$inc" \
+                -Xclang -target-feature -Xclang -packed-fp32-ops $extra $defs \
+                -o "$OUT/$name.$f.o" "$src/$f" 2>&1 | grep -v packed-fp32-ops
+            objs="$objs $OUT/$name.$f.o"
+        done
+        /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/$name.so" $objs
+        rm -f $objs
+    ) &
 done
 wait
 ls "$OUT"
