@@ -6,7 +6,7 @@
 set -e
 OUT=${VAR_OUT:-build/var}
 mkdir -p "$OUT"
-rm -f "$OUT"/*.so
+rm -f "$OUT"/*.so "$OUT"/*.o
 for spec in "$@"; do
     name=${spec%%:*}; defs=${spec#*:}
     src=montecarlo-gated-mil_amd/csrc; inc=include
@@ -25,7 +25,7 @@ for spec in "$@"; do
             [ "$f" = mcgmil.hip ] && extra="-mllvm -amdgpu-sched-strategy=max-ilp"
             /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -c -fPIC -I"$inc" \
                 -Xclang -target-feature -Xclang -packed-fp32-ops $extra $defs \
-                -o "$OUT/$name.$f.o" "$src/$f" 2>&1 | grep -v packed-fp32-ops
+                -o "$OUT/$name.$f.o" "$src/$f" 2>&1 | grep -v packed-fp32-ops || true
             objs="$objs $OUT/$name.$f.o"
         done
         /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/$name.so" $objs
