@@ -57,7 +57,8 @@ def measured_traffic(N, T, B, dtype, shared):
 
 def cpu_baseline(N, T, L, D, C, shared, budget_s):
     """The reference CPU path (torch op sequence incl. dropout RNG), bounded sample."""
-    from oracle import mcdo_ref, synthetic
+    from oracle import mcdo_ref
+    from mcgmil import synthetic
     arrays = synthetic.head_arrays(synthetic.head_state_dict(0, L=L, D=D, C=C, shared=shared), C, shared)
     prm = mcdo_ref.HeadParams(arrays)
     H = synthetic.bag_features(42, N, L)
@@ -115,7 +116,7 @@ def main():
         return
 
     from mcgmil import _lib, ops
-    from oracle import synthetic  # seeded synthetic parameters only (not a compute path)
+    from mcgmil import synthetic
     lib = _lib.load()
 
     N, T, L, D, C = args.n, args.T, 512, 128, 2

@@ -40,7 +40,8 @@ def cpu_baseline(k, T, budget_s=20.0):
     """The same pipeline on the host, bounded: the patcher on the whole image, the ResNet on a
     sample of instances, the head and the maps on a few passes -- each scaled to one image."""
     from mcgmil import MultiHeadGatedAttentionMIL, deactivate_batchnorm
-    from oracle import mcdo_ref, patcher_ref, synthetic
+    from oracle import mcdo_ref, patcher_ref
+    from mcgmil import synthetic
     threads = torch.get_num_threads()
     img = synthetic_mammogram(torch.device("cpu"))
     t0 = time.perf_counter()

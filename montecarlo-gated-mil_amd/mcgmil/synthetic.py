@@ -1,7 +1,8 @@
-"""TEST INFRASTRUCTURE -- seeded synthetic bags and parameters.
+"""Seeded synthetic workload: bags of features and random-init head parameters.
 
-Portable across machines (numpy PCG64), so the committed golden fixtures store only
-outputs; inputs are regenerated from their seeds.
+No dataset or checkpoint can be fetched here, so the benchmark, the tests and the golden
+fixtures all draw their inputs from this module. It is portable across machines (numpy PCG64),
+so the committed fixtures store only outputs; inputs are regenerated from their seeds.
 
   H[n, l]   = |N(0, 1)|                      (post-ReLU/avg-pool ResNet-like features)
   weights   = U(-1/sqrt(fan_in), 1/sqrt(fan_in))  per nn.Linear, like torch's default init

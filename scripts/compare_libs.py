@@ -14,7 +14,7 @@ sys.path.insert(0, REPO)
 
 def run(path, bags, n, T, shared):
     from mcgmil import _lib, ops
-    from oracle import synthetic
+    from mcgmil import synthetic
     _lib._lib = None
     _lib.lib_path = lambda: path
     _lib.load()

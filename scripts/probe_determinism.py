@@ -15,7 +15,7 @@ sys.path[:0] = [REPO, os.path.join(REPO, "montecarlo-gated-mil_amd")]
 
 def main():
     from mcgmil import _lib, ops
-    from oracle import synthetic
+    from mcgmil import synthetic
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from probe_gate import load_variant
     _lib.load()

@@ -27,7 +27,7 @@ def load_variant(path):
 
 def main():
     from mcgmil import _lib, ops
-    from oracle import synthetic
+    from mcgmil import synthetic
     _lib.load()
     # MCGMIL_PROBE_LIBS=a.so,b.so: A/B variant builds of the library in one process
     paths = [p for p in os.environ.get("MCGMIL_PROBE_LIBS", "").split(",") if p]

@@ -21,7 +21,7 @@ PHASES = ["row_table", "prologue", "k_loop", "epilogue", "partials", "barrier", 
 
 def main():
     from mcgmil import _build, _lib, ops
-    from oracle import synthetic
+    from mcgmil import synthetic
     path = os.path.join(REPO, "montecarlo-gated-mil_amd", "mcgmil", "libmcgmil_stamps.so")
     extra = [d for d in os.environ.get("STAMP_DEFINES", "").split(",") if d]
     if extra:

@@ -30,8 +30,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 REF = "/root/reference"
 OUT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "montecarlo-gated-mil_amd"))
 
-from oracle import philox, synthetic  # noqa: E402
+from oracle import philox  # noqa: E402
+from mcgmil import synthetic  # noqa: E402
 
 
 def _install_torchvision_standin():

@@ -5,7 +5,8 @@ import os
 
 import numpy as np
 
-from oracle import mcdo_ref, philox, synthetic
+from oracle import mcdo_ref, philox
+from mcgmil import synthetic
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 META = ("N", "T", "C", "L", "D", "shared", "p_f", "p_a", "h_seed", "w_seed", "mask_seed",

@@ -15,7 +15,8 @@ import pytest
 import torch
 
 from golden_util import GOLDEN, Case, names, nrel
-from oracle import mcdo_ref, philox, synthetic
+from oracle import mcdo_ref, philox
+from mcgmil import synthetic
 
 pytestmark = pytest.mark.gpu
 

@@ -13,7 +13,8 @@ import torch
 
 from golden.make_golden_patcher import synthetic_image
 from golden_util import nrel
-from oracle import mcdo_ref, patcher_ref as P, synthetic
+from oracle import mcdo_ref, patcher_ref as P
+from mcgmil import synthetic
 
 pytestmark = pytest.mark.gpu
 

@@ -28,7 +28,8 @@ def _free_port():
 
 
 def _bag_Y(b):
-    from oracle import mcdo_ref, synthetic
+    from oracle import mcdo_ref
+    from mcgmil import synthetic
     arrays = synthetic.head_arrays(synthetic.head_state_dict(1, C=C, shared=False), C, False)
     H = synthetic.bag_features(500 + b, SIZES[b], L)
     kF, kA = mcdo_ref.masks_for_bag(SEED, b, T, SIZES[b], L, C, 0.1, 0.1)
