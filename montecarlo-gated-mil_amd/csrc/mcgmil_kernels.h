@@ -217,7 +217,8 @@ __device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
                                               float (&part)[MAXC][BM / ROWS], f32x4 zacc,
                                               bool zwave, float* red, float* zred,
                                               const int* rinfo, int one_class, int waves_per_gate,
-                                              bool have_keep, bool keep) {
+                                              bool have_keep, bool keep,
+                                              const float* ba = nullptr) {
     constexpr int RT = BM / ROWS;
     constexpr int NG = 64 / ROWS;                  // lane groups per accumulator tile
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -252,7 +253,7 @@ __device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
 #pragma unroll
         for (int g = 0; g < NG; ++g) s += src[g * BM];
     }
-    s += p.ba[c];
+    s += ba ? ba[c] : p.ba[c];
     const int t = ri[1], n = ri[2], bag = ri[3], Nb = ri[4];
     if (p.keep_att) {
         const size_t abase = (size_t)p.T * p.C * (size_t)p.bag_off[bag];

@@ -136,6 +136,13 @@ def load():
     if not os.path.exists(path):
         raise MCGMILError(f"MI355X extension not built: {path} is missing "
                           "(run __graft_entry__.build() or python -m mcgmil._build)")
+    _lib = bind(path)
+    return _lib
+
+
+def bind(path: str, mcdo_only: bool = False):
+    """dlopen a build of the library and declare its entry points. mcdo_only: a gate-kernel A/B
+    build (scripts/build_variants.sh with GATE_ONLY=1) that holds the MCDO entry points only."""
     L = ctypes.CDLL(path)
     pa = ctypes.POINTER(Args)
     L.mcgmil_abi_version.restype = ctypes.c_int
@@ -156,6 +163,11 @@ def load():
         f = getattr(L, name)
         f.argtypes = [pa, _vp, _vp]
         f.restype = ctypes.c_int
+    if L.mcgmil_args_size() != ctypes.sizeof(Args):
+        raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_args)={L.mcgmil_args_size()} but the "
+                          f"ctypes mirror is {ctypes.sizeof(Args)} bytes")
+    if mcdo_only:
+        return L
     pi = ctypes.POINTER(ImageArgs)
     L.mcgmil_image_args_size.restype = ctypes.c_size_t
     L.mcgmil_tile_grid.argtypes = [pi, _vp, _vp, _vp, _vp]
@@ -206,10 +218,6 @@ def load():
     if L.mcgmil_image_args_size() != ctypes.sizeof(ImageArgs):
         raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_image_args)={L.mcgmil_image_args_size()} "
                           f"but the ctypes mirror is {ctypes.sizeof(ImageArgs)} bytes")
-    if L.mcgmil_args_size() != ctypes.sizeof(Args):
-        raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_args)={L.mcgmil_args_size()} but the "
-                          f"ctypes mirror is {ctypes.sizeof(Args)} bytes")
-    _lib = L
     return L
 
 

@@ -1,10 +1,10 @@
 #!/bin/bash
 # Build A/B variants of libmcgmil.so (one per -D set), in parallel, into $VAR_OUT (default
-# build/var/, git-ignored but shipped to the GPU box with the snapshot).
+# abvar/, git-ignored but shipped to the GPU box with the snapshot; build/ is gpurun-ignored).
 # Usage: bash scripts/build_variants.sh "NAME:-DX=1 -DY=2" "NAME2:..." ...
 #   A NAME of the form "name@REV" builds the sources of git revision REV instead of the tree.
 set -e
-OUT=${VAR_OUT:-build/var}
+OUT=${VAR_OUT:-abvar}
 mkdir -p "$OUT"
 rm -f "$OUT"/*.so "$OUT"/*.o
 for spec in "$@"; do
@@ -19,7 +19,9 @@ for spec in "$@"; do
     # per source, as mcgmil/_build.py: the gate kernels (mcgmil.hip) with the max-ILP scheduler
     (
         objs=""
-        for f in mcgmil.hip mcgmil_image.hip mcgmil_bn.hip mcgmil_conv.hip mcgmil_stem.hip; do
+        srcs="mcgmil.hip mcgmil_image.hip mcgmil_bn.hip mcgmil_conv.hip mcgmil_stem.hip"
+        [ -n "${GATE_ONLY:-}" ] && srcs="mcgmil.hip"   # gate-kernel A/B: the MCDO entry points only
+        for f in $srcs; do
             [ -f "$src/$f" ] || continue
             extra=""
             [ "$f" = mcgmil.hip ] && extra="-mllvm -amdgpu-sched-strategy=max-ilp"

@@ -15,9 +15,7 @@ sys.path.insert(0, REPO)
 def run(path, bags, n, T, shared):
     from mcgmil import _lib, ops
     from mcgmil import synthetic
-    _lib._lib = None
-    _lib.lib_path = lambda: path
-    _lib.load()
+    _lib._lib = _lib.bind(path, mcdo_only=True)
     dev = torch.device("cuda", 0)
     C = 2
     sd = synthetic.head_state_dict(0, C=C, shared=shared)
@@ -33,12 +31,15 @@ def run(path, bags, n, T, shared):
 
 
 def main():
-    a, b = os.environ["MCGMIL_PROBE_LIBS"].split(",")
-    for shared in (False, True):
-        for bags, n, T in ((3, 2048, 100), (5, 300, 7), (2, 4000, 5), (1, 5000, 3)):
-            ra, rb = run(a, bags, n, T, shared), run(b, bags, n, T, shared)
-            same = {k: bool(torch.equal(ra[k], rb[k])) for k in ra}
-            print(json.dumps({"shared": shared, "bags": bags, "n": n, "T": T, "bitwise_equal": same}))
+    libs = os.environ["MCGMIL_PROBE_LIBS"].split(",")
+    a = libs[0]
+    for b in libs[1:]:      # every variant against the first
+        for shared in (False, True):
+            for bags, n, T in ((3, 2048, 100), (5, 300, 7), (2, 4000, 5), (1, 5000, 3)):
+                ra, rb = run(a, bags, n, T, shared), run(b, bags, n, T, shared)
+                same = all(bool(torch.equal(ra[k], rb[k])) for k in ra)
+                print(json.dumps({"a": os.path.basename(a), "b": os.path.basename(b), "shared": shared,
+                                  "bags": bags, "n": n, "T": T, "bitwise_equal": same}))
 
 
 if __name__ == "__main__":

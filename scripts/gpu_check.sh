@@ -44,7 +44,7 @@ for s in $STEPS; do
                 run determinism_pipe 300 env MCGMIL_GATE=pipe python scripts/probe_determinism.py ;;
         probepipe) run probe_pipe 300 env MCGMIL_GATE=pipe python scripts/probe_gate.py ;;
         stamps) run stamps 300 python scripts/probe_stamps.py ;;
-        ab) run ab 300 env MCGMIL_PROBE_LIBS="$(ls -1 build/var/*.so 2>/dev/null | paste -sd, -)" \
+        ab) run ab 300 env MCGMIL_PROBE_LIBS="$(ls -1 abvar/*.so 2>/dev/null | paste -sd, -)" \
                 PROBE_ONLY=philox python scripts/probe_gate.py ;;
         prof)
             rm -rf "$OUT/prof_$TAG"

@@ -19,10 +19,8 @@ import torch  # noqa: E402
 
 
 def load_variant(path):
-    L = ctypes.CDLL(path)
-    for f in ("mcgmil_gate_scores", "mcgmil_workspace_size"):
-        getattr(L, f).restype = ctypes.c_int
-    return L
+    from mcgmil import _lib
+    return _lib.bind(path, mcdo_only=True)
 
 
 def main():
