@@ -55,27 +55,51 @@ def measured_traffic(N, T, B, dtype, shared):
     return None, None
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(N, T, L, D, C, shared, budget_s):
-    """The reference CPU path (torch op sequence incl. dropout RNG), bounded sample."""
+    """The reference CPU path (torch op sequence incl. dropout RNG), bounded sample, on all the
+    host threads torch uses and on one thread (BASELINE.md's plan)."""
     from oracle import mcdo_ref
     from mcgmil import synthetic
     arrays = synthetic.head_arrays(synthetic.head_state_dict(0, L=L, D=D, C=C, shared=shared), C, shared)
     prm = mcdo_ref.HeadParams(arrays)
     H = synthetic.bag_features(42, N, L)
+
+    def timed(budget, max_bags):
+        with torch.no_grad():
+            mcdo_ref.mc_inference_torch_rng(H, prm, T, 0.1, 0.1)   # warm-up
+            n, t0 = 0, time.perf_counter()
+            while True:
+                mcdo_ref.mc_inference_torch_rng(H, prm, T, 0.1, 0.1)
+                n += 1
+                el = time.perf_counter() - t0
+                if el >= budget or n >= max_bags:
+                    return n, el
+
     threads = torch.get_num_threads()
-    with torch.no_grad():
-        mcdo_ref.mc_inference_torch_rng(H, prm, T, 0.1, 0.1)   # warm-up
-        n, t0 = 0, time.perf_counter()
-        while True:
-            mcdo_ref.mc_inference_torch_rng(H, prm, T, 0.1, 0.1)
-            n += 1
-            el = time.perf_counter() - t0
-            if el >= budget_s or n >= 50:
-                break
+    n, el = timed(budget_s, 50)
+    torch.set_num_threads(1)
+    try:
+        n1, el1 = timed(budget_s / 3, 10)
+    finally:
+        torch.set_num_threads(threads)
+    model = cpu_model()
     return {"value": n * T / el, "unit": "bag-samples/s", "cores": threads, "kind": "port",
+            "cpu_model": model,
+            "single_thread": {"value": n1 * T / el1, "unit": "bag-samples/s", "cores": 1,
+                              "ms_per_bag": el1 * 1e3 / n1, "bags": n1},
             "sample": f"{n} bags of N={N}, T={T}, fp32, {'shared' if shared else 'separate'} "
-                      f"attention, torch {torch.__version__} CPU, {threads} threads, "
-                      f"{el * 1e3 / n:.1f} ms/bag"}
+                      f"attention, torch {torch.__version__} CPU, {threads} threads on {model}, "
+                      f"{el * 1e3 / n:.1f} ms/bag; 1 thread: {n1} bags, {el1 * 1e3 / n1:.1f} ms/bag"}
 
 
 def main():

@@ -26,6 +26,26 @@ IMAGENET_MEAN = (0.485, 0.456, 0.406)   # reference utils.py:50-51 (val/test tra
 IMAGENET_STD = (0.229, 0.224, 0.225)
 
 
+def uncertainty_summary(Y: torch.Tensor, prob_mean: Optional[torch.Tensor] = None) -> dict:
+    """The per-bag statistics infer.py / net_utils.py derive from the MC logits Y [T, C]:
+    softmax over classes per pass (infer.py:195), the mean-probability argmax (net_utils.py:
+    207-210), the positive-class mean/median/std (ddof=0)/IQR/min/max over passes
+    (infer.py:47-54, numpy's linear percentiles) and the mean entropy with the reference's
+    +1e-10 (infer.py:56-57). prob_mean: the kernel's P_mean for this bag, if already computed."""
+    probs = torch.softmax(Y, dim=-1)
+    pos = probs[:, -1]
+    q = torch.quantile(pos, torch.tensor([0.25, 0.5, 0.75], device=pos.device, dtype=pos.dtype))
+    ent = -(probs * torch.log(probs + 1e-10)).sum(-1)
+    pm = probs.mean(0) if prob_mean is None else prob_mean
+    return {
+        "probs": probs, "prob_mean": pm, "prediction": int(torch.argmax(pm)),
+        "pos_mean": float(pos.mean()), "pos_median": float(q[1]),
+        "pos_std": float(pos.std(unbiased=False)), "pos_iqr": float(q[2] - q[0]),
+        "pos_min": float(pos.min()), "pos_max": float(pos.max()),
+        "mean_entropy": float(ent.mean()),
+    }
+
+
 def mc_predict_bags(model, bags: Sequence[torch.Tensor], T: int = 50, seed: Optional[int] = None,
                     bag_ids: Optional[Sequence[int]] = None) -> List[dict]:
     """bags: list of feature matrices H_b [N_b, L] on one HIP device."""
@@ -49,19 +69,10 @@ def mc_predict_bags(model, bags: Sequence[torch.Tensor], T: int = 50, seed: Opti
     res = []
     for b, n in enumerate(sizes):
         Y = out["Y"][b]                                   # [T, C]
-        probs = torch.softmax(Y, dim=-1)
-        pos = probs[:, -1]
-        q = torch.quantile(pos, torch.tensor([0.25, 0.5, 0.75], device=pos.device))
-        ent = -(probs * torch.log(probs + 1e-10)).sum(-1)
-        res.append({
-            "Y": Y, "probs": probs, "prob_mean": out["P_mean"][b],
-            "prediction": int(torch.argmax(out["P_mean"][b])),
-            "pos_mean": float(pos.mean()), "pos_median": float(q[1]),
-            "pos_std": float(pos.std(unbiased=False)), "pos_iqr": float(q[2] - q[0]),
-            "pos_min": float(pos.min()), "pos_max": float(pos.max()),
-            "mean_entropy": float(ent.mean()),
-            "A_mean": Am[b].view(C, n), "A_var": Av[b].view(C, n),
-        })
+        r = {"Y": Y}
+        r.update(uncertainty_summary(Y, out["P_mean"][b]))
+        r.update({"A_mean": Am[b].view(C, n), "A_var": Av[b].view(C, n)})
+        res.append(r)
     return res
 
 

@@ -150,12 +150,67 @@ def dump_head_keys():
         json.dump(keys, f, indent=1, sort_keys=True)
 
 
+def torchvision_resnet_keys(depth):
+    """State-dict keys/shapes of torchvision's resnet18/34 (BasicBlock; torchvision
+    models/resnet.py ResNet._make_layer) with fc replaced by an Identity (reference
+    model.py:179) and every BatchNorm's running statistics removed by deactivate_batchnorm
+    (reference main.py:62 before training, infer.py:154 before loading): weight, bias and
+    num_batches_tracked remain. torchvision is not installed here, so this enumerates the
+    architecture; it is the backbone half of the checkpoint ABI the build commits to."""
+    blocks = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3]}[depth]
+    keys = {"conv1.weight": [64, 3, 7, 7]}
+
+    def bn(prefix, c):
+        keys.update({prefix + ".weight": [c], prefix + ".bias": [c], prefix + ".num_batches_tracked": []})
+    bn("bn1", 64)
+    inplanes = 64
+    for li, (planes, nb) in enumerate(zip((64, 128, 256, 512), blocks), start=1):
+        for j in range(nb):
+            pre = f"layer{li}.{j}"
+            keys[pre + ".conv1.weight"] = [planes, inplanes, 3, 3]
+            bn(pre + ".bn1", planes)
+            keys[pre + ".conv2.weight"] = [planes, planes, 3, 3]
+            bn(pre + ".bn2", planes)
+            if j == 0 and (li > 1):
+                keys[pre + ".downsample.0.weight"] = [planes, inplanes, 1, 1]
+                bn(pre + ".downsample.1", planes)
+            inplanes = planes
+    return keys
+
+
+def dump_checkpoint_keys():
+    """Full key/shape list of a reference checkpoint (main.py:92-94 torch.save of the module's
+    state_dict): the head half from the reference module itself, the backbone half from
+    torchvision_resnet_keys (under feature_extractor.)."""
+    import json
+    out = {}
+    for depth in (18, 34):
+        for shared in (False, True):
+            sd = synthetic.head_state_dict(0, shared=shared)
+            m = build_reference(2, shared, sd, 0.1, 0.1)
+            head = {k: list(v.shape) for k, v in m.state_dict().items()
+                    if not k.startswith("feature_extractor")}
+            keys = {"feature_extractor." + k: v for k, v in torchvision_resnet_keys(depth).items()}
+            keys.update(head)
+            out[f"r{depth}_{'shared' if shared else 'separate'}"] = keys
+    with open(os.path.join(OUT, "reference_checkpoint_keys.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def main():
     if not os.path.isdir(REF):
         raise SystemExit("make_golden.py needs the reference checkout at /root/reference")
     _install_torchvision_standin()
     torch.set_num_threads(8)
+    only = set(sys.argv[1:])     # e.g. "big ckpt": regenerate just those groups
+    if only:
+        if "ckpt" in only:
+            dump_checkpoint_keys()
+        if "big" in only:
+            big_cases()
+        return
     dump_head_keys()
+    dump_checkpoint_keys()
     # (1) small bags, T=1 and T=4, shared and separate
     for shared in (False, True):
         tag = "shared" if shared else "sep"
@@ -190,6 +245,15 @@ def main():
              bag_ctr=1, bf16=True, full_A=False)
     run_case("cfg3_N2048_T100_shared_bf16in", N=2048, T=100, shared=True, h_seed=43, w_seed=0,
              mask_seed=42, bag_ctr=1, bf16=True, full_A=False)
+    big_cases()
+
+
+def big_cases():
+    """Bags above 4096 instances (softmax_pool_kernel's streaming branch): the reference's
+    inference settings (config.yml:31,34: overlap 0.75) give up to ~5.8k tiles per image."""
+    run_case("big_N5500_T4_sep", N=5500, T=4, h_seed=50, w_seed=51, mask_seed=52, bag_ctr=3)
+    run_case("big_N4100_T3_shared", N=4100, T=3, shared=True, h_seed=53, w_seed=54, mask_seed=55,
+             bag_ctr=9)
 
 
 if __name__ == "__main__":

@@ -383,3 +383,71 @@ def test_head_shapes_match_oracle(cuda, L, D, C, shared, dtype):
         Yr, Ar = mcdo_ref.mc_inference(Hs_ref[b], prm, kF, kA, 0.2, 0.1)
         np.testing.assert_allclose(Y[b], Yr[:, 0].numpy(), atol=tol["Y"])
         assert nrel(A[b].numpy().reshape(T, C, n), Ar[:, 0].numpy()) <= tol["A"]
+
+
+# ------------------------------------------------------------------ caller statistics (a11)
+@pytest.mark.parametrize("name", ["cfg2_N512_T30_sep", "cfg2_N512_T30_shared"])
+def test_mc_predict_bags_caller_stats(cuda, name):
+    """mcgmil.infer.mc_predict_bags (the infer.py / net_utils.mc_test counterpart) against the
+    numpy restatement of infer.py:47-57 / net_utils.py:205-210 on the reference's own outputs."""
+    from mcgmil import infer
+    from oracle import caller_stats
+    case = Case(name)
+    m = _module(case, cuda)
+    H, _, _ = case.inputs()
+    res = infer.mc_predict_bags(m, [torch.from_numpy(H).to(cuda)], T=case.T, seed=case.mask_seed,
+                                bag_ids=[case.bag_ctr])[0]
+    want = caller_stats.caller_stats(case.z["Y"][:, 0], case.z["A"][:, 0])
+    np.testing.assert_allclose(res["Y"].cpu().numpy(), case.z["Y"][:, 0], atol=TOL32["Y"])
+    np.testing.assert_allclose(res["probs"].cpu().numpy(), want["probs"], atol=1e-5)
+    np.testing.assert_allclose(res["prob_mean"].cpu().numpy(), want["prob_mean"], atol=TOL32["P_mean"])
+    assert res["prediction"] == want["prediction"]
+    for k in ("pos_mean", "pos_median", "pos_std", "pos_iqr", "pos_min", "pos_max", "mean_entropy"):
+        assert abs(res[k] - want[k]) <= 1e-5, (k, res[k], want[k])
+    assert nrel(res["A_mean"].cpu().numpy(), want["A_mean"]) <= TOL32["A_mean"]
+    assert nrel(res["A_var"].cpu().numpy(), want["A_var"]) <= TOL32["A_var"]
+
+
+# ------------------------------------------------------------------ BASELINE config 4 workload
+def test_cfg4_ragged_batch(cuda):
+    """Config 4's workload on one GPU: 64 bags with N_b drawn as BASELINE config 4 draws them
+    (rng(0).integers(256, 2049)), T=100, bf16, ONE varlen launch with global bag ids (the ids a
+    rank of the 8-GPU run would pass). The smallest, the largest and two other bags are checked
+    against the oracle (bf16-rounded inputs, masks from the C Philox), every bag through the
+    size-independent properties, and the launch is bitwise repeatable."""
+    from mcgmil import ops
+    sizes = np.random.default_rng(0).integers(256, 2049, 4096)[:64].tolist()
+    ids = list(range(1000, 1064))
+    T, C, L, D, seed = 100, 2, 512, 128, 42
+    sd = synthetic.head_state_dict(0, L=L, D=D, C=C, shared=False)
+    arrays = synthetic.head_arrays(sd, C, False)
+    prm = mcdo_ref.HeadParams(synthetic.head_arrays(synthetic.round_state_dict_bf16(sd), C, False))
+    Hs = [synthetic.bf16_round(synthetic.bag_features(2000 + b, n, L)) for b, n in enumerate(sizes)]
+    H = torch.from_numpy(np.concatenate(Hs)).to(cuda).bfloat16()
+    offs = ops.bag_offsets_tensor(sizes, cuda)
+    bid = torch.tensor(ids, dtype=torch.int32, device=cuda)
+    out = ops.mcdo_forward(H, offs, head_on(arrays, cuda), T, p_feat=0.1, p_att=0.1, seed=seed,
+                           bag_ids=bid, return_stats=True)
+    again = ops.mcdo_forward(H, offs, head_on(arrays, cuda), T, p_feat=0.1, p_att=0.1, seed=seed,
+                             bag_ids=bid, return_stats=True)
+    for k in out:
+        assert torch.equal(out[k], again[k]), k
+    Y = out["Y"].cpu().numpy()
+    A = ops.split_bags(out["A"].cpu(), sizes, T * C)
+    Am = ops.split_bags(out["A_mean"].cpu(), sizes, C)
+    Av = ops.split_bags(out["A_var"].cpu(), sizes, C)
+    for b, n in enumerate(sizes):                         # properties, every bag
+        Ab = A[b].view(T, C, n)
+        assert torch.allclose(Ab.sum(-1), torch.ones(T, C), atol=1e-5)
+        assert torch.allclose(Am[b].view(C, n), Ab.mean(0), atol=1e-7)
+        assert torch.allclose(Av[b].view(C, n), Ab.var(0), rtol=1e-4, atol=1e-12)
+    P = torch.softmax(out["Y"], -1).mean(1)
+    assert torch.allclose(out["P_mean"], P, atol=1e-6)
+    check = sorted({int(np.argmin(sizes)), int(np.argmax(sizes)), 7, 40})
+    for b in check:                                        # against the oracle
+        n = sizes[b]
+        kF, kA = mcdo_ref.masks_for_bag(seed, ids[b], T, n, L, C, 0.1, 0.1)
+        Yr, Ar = mcdo_ref.mc_inference(Hs[b], prm, kF, kA, 0.1, 0.1)
+        np.testing.assert_allclose(Y[b], Yr[:, 0].numpy(), atol=TOL_BF16_IN["Y"])
+        assert nrel(A[b].numpy().reshape(T, C, n), Ar[:, 0].numpy()) <= TOL_BF16_IN["A"]
+        assert nrel(Am[b].numpy().reshape(C, n), Ar[:, 0].mean(0).numpy()) <= TOL_BF16_IN["A_mean"]

@@ -101,3 +101,32 @@ def test_torch_library_op_has_no_cpu_path():
     with pytest.raises(ValueError, match="CUDA"):
         torch.ops.mcgmil.mcdo_forward(torch.zeros(R, L), torch.tensor([0, R], dtype=torch.int32),
                                       *head, 2, 0.1, 0.1, 1, 0, 0)
+
+
+@pytest.mark.parametrize("cfg", ["r18_separate", "r18_shared", "r34_separate"])
+def test_reference_checkpoint_loads_strictly(tmp_path, cfg):
+    """A reference checkpoint (main.py:92-94: torch.save of the module's state_dict after
+    deactivate_batchnorm, main.py:62) with every key the reference module has -- head keys taken
+    from the reference itself, backbone keys torchvision's (tests/golden/make_golden.py
+    dump_checkpoint_keys) -- goes through torch.save / torch.load(weights_only=True) and loads
+    with strict=True into the drop-in module, as infer.py:154-159 does; every value lands."""
+    from mcgmil import MultiHeadGatedAttentionMIL, deactivate_batchnorm
+    spec = json.load(open(os.path.join(GOLDEN, "reference_checkpoint_keys.json")))[cfg]
+    g = torch.Generator().manual_seed(0)
+    sd = {k: (torch.zeros((), dtype=torch.int64) if k.endswith("num_batches_tracked")
+              else torch.randn(shape, generator=g)) for k, shape in spec.items()}
+    path = tmp_path / "ckpt.pth"
+    torch.save(sd, path)
+    loaded = torch.load(path, map_location="cpu", weights_only=True)
+    depth, att = cfg.split("_")
+    # pretrained=False builds resnet18 whatever the backbone (reference model.py:177-178);
+    # infer.py constructs with the default pretrained=True (offline here: random init + warning)
+    with pytest.warns(UserWarning):
+        m = MultiHeadGatedAttentionMIL(num_classes=2, backbone=depth, pretrained=True,
+                                       shared_attention=(att == "shared"))
+    m.apply(deactivate_batchnorm)                                 # infer.py:154
+    assert {k: list(v.shape) for k, v in m.state_dict().items()} == spec
+    m.load_state_dict(loaded, strict=True)                        # infer.py:159
+    own = m.state_dict()
+    for k, v in sd.items():
+        assert torch.equal(own[k], v), k
