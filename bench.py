@@ -116,6 +116,8 @@ def main():
                     help="cfg3: --bags bags of N=--n per GPU (weak scaling, the headline); "
                          "cfg4: 4096 bags N~U(256,2048) LPT-sharded over the GPUs (strong scaling); "
                          "cfg5: end-to-end image -> patcher -> ResNet-18 -> head -> maps (bench_cfg5.py)")
+    ap.add_argument("--features", choices=["bf16", "fp32"], default="bf16",
+                    help="cfg5 only: precision of the instances / ResNet / head operands")
     ap.add_argument("--dist-backend", default="nccl", help=argparse.SUPPRESS)   # rehearsal: gloo
     ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)  # ranks on cuda:0
     ap.add_argument("--cpu-budget", type=float, default=12.0)

@@ -1,9 +1,17 @@
 """BASELINE config 5 (bench.py --workload cfg5): end-to-end per-image MCDO inference on one
 MI355X per rank -- on-GPU ImagePatcher (7036 x 2800 synthetic mammogram, 3 channels, 224 px
-tiles, overlap 0.5, empty_thresh 0.5, the dataset's ImageNet Normalize fused) -> ResNet-18
-feature extractor (PyTorch-ROCm, bf16 autocast, batch-statistics BN over the bag) -> fused
-MCDO head kernel (T=100, separate attention, bf16 operands) -> softmax probabilities ->
-attention-map mean/std over passes on the image grid (infer.py:187-219 without the plotting).
+tiles at the reference's inference settings, overlap_val_test 0.75 and empty_threshold 0.75
+(config.yml:31,34): 5,781 tiles, ~1,500 kept, the dataset's ImageNet Normalize fused) ->
+ResNet-18 feature extractor (batch-statistics BN over the bag) -> MCDO head kernel (T=100,
+separate attention) -> softmax probabilities -> attention-map mean/std over passes on the image
+grid (infer.py:187-219 without the plotting).
+
+Two precisions (--features):
+  fp32  the reference's precision end to end: fp32 instances, the PyTorch-ROCm ResNet layers
+        (MIOpen convolutions; this build's HIP convolutions are bf16-only), fp32 head operands;
+  bf16  bf16 instances, the build's HIP backbone under autocast, bf16 head operands. The run
+        also pushes its last image through the fp32 pipeline (same seed, untimed) and reports
+        the drift of prob_mean / A_mean / Y against it.
 
 A step = one image through all of that, the image already resident in HBM. Each rank runs its
 own image per step (images are independent: weak scaling, no collective on the data path).
@@ -21,7 +29,8 @@ import torch
 import torch.distributed as dist
 
 RESNET18_GFLOP = 3.64          # per 3 x 224 x 224 instance (2 x 1.82 GMAC)
-H_IMG, W_IMG, PS, OVERLAP, THRESH = 7036, 2800, 224, 0.5, 0.5
+H_IMG, W_IMG, PS, OVERLAP, THRESH = 7036, 2800, 224, 0.75, 0.75   # config.yml:31,34
+BLOB = (0.30, 0.58)     # semi-axes of the breast region (fractions of H, W): k = 1,507 tiles kept
 
 
 def synthetic_mammogram(dev, seed=5):
@@ -30,7 +39,7 @@ def synthetic_mammogram(dev, seed=5):
     g = torch.Generator(device=dev).manual_seed(seed)
     yy = torch.arange(H_IMG, device=dev, dtype=torch.float32)[:, None]
     xx = torch.arange(W_IMG, device=dev, dtype=torch.float32)[None, :]
-    blob = 1 - ((yy - 0.5 * H_IMG) / (0.45 * H_IMG)) ** 2 - (xx / (0.85 * W_IMG)) ** 2
+    blob = 1 - ((yy - 0.5 * H_IMG) / (BLOB[0] * H_IMG)) ** 2 - (xx / (BLOB[1] * W_IMG)) ** 2
     noise = torch.rand(H_IMG, W_IMG, device=dev, generator=g) * 0.05
     img = torch.where(blob > 0, blob + noise, torch.zeros_like(blob))
     return img[None].repeat(3, 1, 1).contiguous()
@@ -86,19 +95,22 @@ def run(args, world, rank, dev, peak_tflops):
     from mcgmil.infer import mc_predict_image
     from mcgmil.patcher import ImagePatcher
     T = args.T
+    bf16 = args.features == "bf16"
     torch.manual_seed(0)
     model = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=bool(args.shared))
     model.apply(deactivate_batchnorm)                       # infer.py:154
-    model.compute_dtype = torch.bfloat16
+    model.compute_dtype = torch.bfloat16 if bf16 else torch.float32
     model.to(dev).eval()
     model.feature_extractor.to(memory_format=torch.channels_last)
     patcher = ImagePatcher(patch_size=PS, overlap=OVERLAP, empty_thresh=THRESH)
     patcher.get_tiles(H_IMG, W_IMG)
     img = synthetic_mammogram(dev, seed=5 + rank)
     stream = torch.cuda.current_stream(dev)
+    fdt = torch.bfloat16 if bf16 else None
 
     def step(i, events=None):
-        return mc_predict_image(model, patcher, img, T=T, seed=1000 * rank + i, events=events)
+        return mc_predict_image(model, patcher, img, T=T, seed=1000 * rank + i, events=events,
+                                features_dtype=fdt)
 
     for i in range(args.warmup):
         out = step(i)
@@ -129,22 +141,44 @@ def run(args, world, rank, dev, peak_tflops):
     feat_tflops = k * RESNET18_GFLOP / stage_ms["features"]         # GFLOP / ms = TFLOP/s
     if rank != 0:
         return None
+    drift = None
+    if bf16:      # the same image and seed through the fp32 pipeline (untimed)
+        seed = 1000 * rank + args.warmup + args.steps - 1
+        ob = step(args.warmup + args.steps - 1)
+        model.compute_dtype = torch.float32
+        of = mc_predict_image(model, patcher, img, T=T, seed=seed, features_dtype=None)
+        model.compute_dtype = torch.bfloat16
+        am_f, am_b = of["A_mean"].double(), ob["A_mean"].double()
+        drift = {"prob_mean_abs": float((ob["prob_mean"] - of["prob_mean"]).abs().max()),
+                 "A_mean_nrel": float((am_b - am_f).abs().max() / am_f.abs().max()),
+                 "A_var_nrel": float((ob["A_var"].double() - of["A_var"].double()).abs().max()
+                                     / of["A_var"].double().abs().max()),
+                 "Y_abs": float((ob["Y"] - of["Y"]).abs().max()),
+                 "features_nrel": float((ob["features"].double() - of["features"].double()).abs().max()
+                                        / of["features"].double().abs().max())}
     cpu = None if args.no_cpu_baseline else cpu_baseline(k, T)
     images = world * args.steps
     return {
         "metric": "end-to-end images/sec x MCDO-samples (T=100), config 5", "value": images * T / el,
         "unit": "bag-samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "bf16",
+        "vs_baseline": None, "dtype": args.features,
         "data": "synthetic 7036x2800 mammogram-like image, random-init ResNet-18 and head",
         "config": {"workload": f"BASELINE config 5: {H_IMG}x{W_IMG} image -> {PS}px tiles "
-                               f"(overlap {OVERLAP}, {len(patcher.tiles)} tiles, k={k} kept) -> "
-                               f"ResNet-18 bf16 -> MCDO head T={T} -> attention map mean/std",
+                               f"(overlap {OVERLAP}, empty_thresh {THRESH}, {len(patcher.tiles)} "
+                               f"tiles, k={k} kept) -> ResNet-18 {args.features} -> MCDO head "
+                               f"T={T} -> attention map mean/std",
                    "images_per_s": images / el, "instances_per_bag": k, "T": T,
+                   "features": ("bf16: HIP backbone (autocast), bf16 head operands" if bf16 else
+                                "fp32: PyTorch-ROCm ResNet layers (MIOpen), fp32 head operands"),
+                   "drift_vs_fp32_pipeline": drift,
                    "stage_ms": stage_ms, "parallelism": f"one image per GPU per step, {world} GPU(s)"},
-        "roofline": {"bound": "mfma", "achieved": feat_tflops, "peak": peak_tflops, "unit": "TFLOP/s",
-                     "frac": feat_tflops / peak_tflops, "traffic": None,
-                     "kernel": "ResNet-18 feature extractor (stem + implicit-GEMM convolutions + fused BN, the dominant stage)",
+        "roofline": {"bound": "mfma", "achieved": feat_tflops,
+                     "peak": peak_tflops if bf16 else 157.3, "unit": "TFLOP/s",
+                     "frac": feat_tflops / (peak_tflops if bf16 else 157.3), "traffic": None,
+                     "kernel": "ResNet-18 feature extractor (the dominant stage): " +
+                               ("stem + implicit-GEMM convolutions + fused BN (HIP, bf16)" if bf16 else
+                                "torch/MIOpen fp32 layers"),
                      "algorithmic_tflop_per_launch": k * RESNET18_GFLOP / 1e3},
         "cpu_baseline": cpu,
     }

@@ -85,6 +85,14 @@ def test_mc_predict_image_stages(cuda, shared):
     torch.testing.assert_close(out["att_std"].cpu(), std, rtol=0, atol=STAT_ATOL)
 
 
+# bf16 pipeline (bf16 instances, HIP backbone under autocast, bf16 head operands) against the
+# fp32 pipeline on the same image and seed (random-init ResNet-18, so the bf16 backbone moves
+# the features by ~3%). Measured: this test's image 4.6e-4 prob_mean, 1.5e-2 A_mean nrel,
+# 4.6e-3 Y; the full config-5 image (k = 1,507, profiles/r02/bench_cfg5_bf16.log) 3.2e-5,
+# 9.9e-3, 7.2e-4. The bounds leave 3-4x headroom over the larger of the two.
+DRIFT_PROB_MEAN, DRIFT_A_MEAN, DRIFT_Y = 2e-3, 5e-2, 2e-2
+
+
 def test_mc_predict_image_bf16_features(cuda):
     """bf16 instances + autocast ResNet: predictions close to the fp32 pipeline."""
     from mcgmil import MultiHeadGatedAttentionMIL, deactivate_batchnorm
@@ -100,5 +108,9 @@ def test_mc_predict_image_bf16_features(cuda):
     a = mc_predict_image(model, patcher, img, T=20, seed=3, features_dtype=None)
     b = mc_predict_image(model, patcher, img, T=20, seed=3, features_dtype=torch.bfloat16)
     assert np.array_equal(a["tiles_indices"], b["tiles_indices"])
-    assert (a["prob_mean"] - b["prob_mean"]).abs().max() < 2e-2
+    dp = float((a["prob_mean"] - b["prob_mean"]).abs().max())
+    am = float((a["A_mean"] - b["A_mean"]).abs().max() / a["A_mean"].abs().max())
+    dy = float((a["Y"] - b["Y"]).abs().max())
+    print(f"bf16-vs-fp32 pipeline drift: prob_mean {dp:.3g}, A_mean nrel {am:.3g}, Y {dy:.3g}")
+    assert dp < DRIFT_PROB_MEAN and am < DRIFT_A_MEAN and dy < DRIFT_Y
     assert torch.isfinite(b["att_mean"]).all() and torch.isfinite(b["att_std"]).all()
