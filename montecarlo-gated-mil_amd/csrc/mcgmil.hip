@@ -11,7 +11,6 @@
 #include "mcgmil_error.h"
 #include "mcgmil_kernels.h"
 #include "mcgmil_gate_pp.h"
-#include "mcgmil_gate_pipe2.h"
 
 namespace mcgmil_detail {
 
@@ -171,21 +170,6 @@ int launch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_pipe_kernel launch");
 }
 
-template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE>
-int launch_gate_pipe2(const mcgmil::GateParams& gp, hipStream_t s) {
-    auto* k = &mcgmil::gate_pipe2_kernel<E, PPW, MAXC, REPLAY, ONE>;
-    static std::once_flag once;
-    std::call_once(once, [&] { raise_lds_cap(k); });
-    const long long tiles = (gp.total_samples + mcgmil::kPipeBM - 1) / mcgmil::kPipeBM;
-    if (tiles == 0) return MCGMIL_OK;
-    if (gp.uniform_rows <= 0)
-        if (int rc = launch_plan(gp, mcgmil::kPipeBM, s)) return rc;
-    const size_t lds = mcgmil::pipe2_lds_bytes<E, MAXC>(gp.G, gp.D, gp.C);
-    hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(mcgmil::kGateThreads), lds, s, gp);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_pipe2_kernel launch");
-}
-
 template <typename E, int RT, int PPW, int MAXC, bool REPLAY, bool ONE>
 int launch_gate_pp(const mcgmil::GateParams& gp, hipStream_t s) {
     constexpr int BM = 16 * RT;
@@ -203,28 +187,19 @@ int launch_gate_pp(const mcgmil::GateParams& gp, hipStream_t s) {
 // Kernel choice for bf16 heads of up to 16 gate tile pairs (measured, config 3, MI355X):
 // separate heads (P = 16) run the one-workgroup-per-CU gate_pipe_kernel (914 vs 853 TFLOP/s),
 // shared heads (P = 8) the two-workgroups-per-CU gate_pp_kernel (820 vs 781).
-// MCGMIL_GATE=pipe / pp forces one of them (A/B timing). gate_pipe2_kernel (mcgmil_gate_pipe2.h)
-// is the latency-chain variant of gate_pipe_kernel: bitwise the same outputs, measured 2.5%
-// slower (profiles/r02/ab_pipe2.log), so it runs only with MCGMIL_GATE=pipe2 or -DMCGMIL_PIPE_V1=0.
+// MCGMIL_GATE=pipe / pp forces one of them (A/B timing). Variants measured slower and removed
+// are listed with their numbers in profiles/r02/gate_ab.log and DESIGN.md §5.
+#ifndef MCGMIL_GATE_DEFAULT
+#define MCGMIL_GATE_DEFAULT 0       // A/B builds: 1 pipe, 2 pp
+#endif
 int gate_mode() {   // 0 auto, 1 pipe, 2 pp
     static const int mode = [] {
         const char* e = getenv("MCGMIL_GATE");
-        if (e && (strcmp(e, "pipe") == 0 || strcmp(e, "pipe1") == 0)) return 1;
+        if (e && strcmp(e, "pipe") == 0) return 1;
         if (e && strcmp(e, "pp") == 0) return 2;
-        return 0;
+        return MCGMIL_GATE_DEFAULT;
     }();
     return mode;
-}
-bool pipe_v1() {
-#ifndef MCGMIL_PIPE_V1
-#define MCGMIL_PIPE_V1 1
-#endif
-    static const bool v1 = [] {
-        const char* e = getenv("MCGMIL_GATE");
-        if (e && strcmp(e, "pipe2") == 0) return false;
-        return MCGMIL_PIPE_V1 || (e && strcmp(e, "pipe1") == 0);
-    }();
-    return v1;
 }
 
 template <int RT, int PPW, int MAXC>
@@ -242,16 +217,10 @@ int dispatch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
     const bool replay = gp.keep_feat != nullptr;
     // separate heads whose gate tile pairs split evenly over the waves: one class per wave
     const bool one = gp.G > 1 && gp.G == gp.C && (gp.D / 16) % PPW == 0;
-    if (pipe_v1()) {
-        if (replay) return one ? launch_gate_pipe<E, PPW, MAXC, true, true>(gp, s)
-                               : launch_gate_pipe<E, PPW, MAXC, true, false>(gp, s);
-        return one ? launch_gate_pipe<E, PPW, MAXC, false, true>(gp, s)
-                   : launch_gate_pipe<E, PPW, MAXC, false, false>(gp, s);
-    }
-    if (replay) return one ? launch_gate_pipe2<E, PPW, MAXC, true, true>(gp, s)
-                           : launch_gate_pipe2<E, PPW, MAXC, true, false>(gp, s);
-    return one ? launch_gate_pipe2<E, PPW, MAXC, false, true>(gp, s)
-               : launch_gate_pipe2<E, PPW, MAXC, false, false>(gp, s);
+    if (replay) return one ? launch_gate_pipe<E, PPW, MAXC, true, true>(gp, s)
+                           : launch_gate_pipe<E, PPW, MAXC, true, false>(gp, s);
+    return one ? launch_gate_pipe<E, PPW, MAXC, false, true>(gp, s)
+               : launch_gate_pipe<E, PPW, MAXC, false, false>(gp, s);
 }
 
 template <typename E, int MAXC>

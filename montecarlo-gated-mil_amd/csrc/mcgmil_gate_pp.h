@@ -134,7 +134,11 @@ __global__ __launch_bounds__(kPPThreads, 2) void gate_pp_kernel(const GateParams
     // are prefetched into hn and step s+1 (from h, loaded a step earlier) is staged into `nxt`.
     auto kstep = [&](int s, const E* cur, E* nxt, Frag<E> (&w)[NJ], Frag<E> (&wn)[NJ], Frag<E>& zc,
                      Frag<E>& zn, const Raw<E> (&h)[CH], Raw<E> (&hn)[CH]) {
+#if MCGMIL_DIAG & 64   // ablation (timing only): every step reloads the weights of step 0 (L1 hits)
+        const int s1 = 0;
+#else
         const int s1 = s + 1 < KS ? s + 1 : KS - 1;
+#endif
         const int s2 = s + 2 < KS ? s + 2 : KS - 1;
 #pragma unroll
         for (int i = 0; i < CH; ++i) hn[i] = load_raw(hsrc[i] + (size_t)s2 * 32);
@@ -148,14 +152,18 @@ __global__ __launch_bounds__(kPPThreads, 2) void gate_pp_kernel(const GateParams
                 if (MCGMIL_PP_XRELOAD) x[rt] = load_frag(cur + (size_t)(rt * 64 + lane) * 8);
                 acc[rt][j] = mma(w[j], x[rt], acc[rt][j]);
             }
+#if !(MCGMIL_DIAG & 2)   // ablation (timing only): no weight reloads
             wn[j] = load_frag_buf<E>(wrs, lane_b, wsoff[j] + (uint32_t)s1 * kStepBytes);
+#endif
         }
 #pragma unroll
         for (int i = 0; i < CH; ++i) {   // classifier tile of row tile wave + 4 i
             const Frag<E> xz = load_frag(cur + (size_t)((wave + kPPWaves * i) * 64 + lane) * 8);
             zacc[i] = mma(zc, xz, zacc[i]);
         }
+#if !(MCGMIL_DIAG & 2)
         zn = load_frag_buf<E>(wrs, lane_b, zsoff + (uint32_t)s1 * kStepBytes);
+#endif
         stage(s + 1, h, nxt);   // step KS lands in the idle slot and is never read
         if constexpr (sizeof(E) == 2 && MCGMIL_PP_PIN) {
 #pragma unroll
@@ -192,6 +200,9 @@ __global__ __launch_bounds__(kPPThreads, 2) void gate_pp_kernel(const GateParams
     // MFMAs take the zero accumulators as an inline constant (no copies into the loop).
     kstep(0, Xs, Xs + SLOT, wA, wB, zA, zB, hB, hA);
     kstep(1, Xs + SLOT, Xs, wB, wA, zB, zA, hA, hB);
+#if MCGMIL_DIAG & 16   // ablation (timing only): 2 of the KS K steps
+    if (KS > 1000)
+#endif
     for (int s = 2; s < KS; s += 2) {
         kstep(s, Xs, Xs + SLOT, wA, wB, zA, zB, hB, hA);
         kstep(s + 1, Xs + SLOT, Xs, wB, wA, zB, zA, hA, hB);

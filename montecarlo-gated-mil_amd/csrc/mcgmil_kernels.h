@@ -142,6 +142,10 @@ __device__ __forceinline__ float gated_product_scaled(float ax, float by) {
     return (1.0f - a) * __builtin_amdgcn_rcpf(fmaf(ia, b, ia));
 }
 
+#ifndef MCGMIL_DIAG
+#define MCGMIL_DIAG 0               // ablation bits for timing studies (never in the product)
+#endif
+
 constexpr float kM2Log2e = -2.8853900817779268f;   // -2 / ln 2
 constexpr float kMLog2e = -1.4426950408889634f;    // -1 / ln 2
 
@@ -181,6 +185,10 @@ __device__ __forceinline__ void fold_pairs(const GateParams& p, const f32x4 (&ac
                 const float ax = fmaf(acc[rt][2 * jp][v], av_s, bvv[v]);
                 const float by = fmaf(acc[rt][2 * jp + 1][v], au_s, buv[v]);
                 if constexpr (ONE_CLASS) {
+#if MCGMIL_DIAG & 8   // ablation (timing only): no transcendentals in the epilogue
+                    part[0][rt] = fmaf(fmaf(ax, coef[0][v], by), ax, part[0][rt]);
+                    continue;
+#endif
                     // wa (1 - a) / ((1 + a)(1 + b)) as two FMAs around the reciprocal
                     const float a = __builtin_amdgcn_exp2f(fminf(fmaxf(ax, -43.280851226668903f),
                                                                  43.280851226668903f));
@@ -217,8 +225,7 @@ __device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
                                               float (&part)[MAXC][BM / ROWS], f32x4 zacc,
                                               bool zwave, float* red, float* zred,
                                               const int* rinfo, int one_class, int waves_per_gate,
-                                              bool have_keep, bool keep,
-                                              const float* ba = nullptr) {
+                                              bool have_keep, bool keep) {
     constexpr int RT = BM / ROWS;
     constexpr int NG = 64 / ROWS;                  // lane groups per accumulator tile
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -253,7 +260,7 @@ __device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
 #pragma unroll
         for (int g = 0; g < NG; ++g) s += src[g * BM];
     }
-    s += ba ? ba[c] : p.ba[c];
+    s += p.ba[c];
     const int t = ri[1], n = ri[2], bag = ri[3], Nb = ri[4];
     if (p.keep_att) {
         const size_t abase = (size_t)p.T * p.C * (size_t)p.bag_off[bag];
@@ -343,9 +350,6 @@ constexpr int kPipeBM = 128;
 #define MCGMIL_VPM 2
 #endif
 constexpr int VPM = MCGMIL_VPM;   // VALU instructions scheduled after each MFMA in a K step
-#ifndef MCGMIL_DIAG
-#define MCGMIL_DIAG 0               // ablation bits for timing studies (never in the product)
-#endif
 #ifndef MCGMIL_SCHED
 #define MCGMIL_SCHED 0
 #endif
@@ -513,6 +517,9 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     // the 132 zeroed accumulators are made on the way into the loop.
     kstep(0, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA);
     kstep(1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB);
+#if MCGMIL_DIAG & 16   // ablation (timing only): 2 of the KS K steps
+    if (KS > 1000)
+#endif
     for (int s = 2; s < KS; s += 2) {
         kstep(s, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA);
         kstep(s + 1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB);

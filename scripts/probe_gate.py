@@ -38,8 +38,9 @@ def main():
     iters = 5
     variants = []
     for name in libs:
-        for dtype in (torch.bfloat16, torch.float32):
-            for shared in (False, True):
+        sep_only = os.environ.get("PROBE_SEP_ONLY") == "1"      # bf16 separate heads only
+        for dtype in ((torch.bfloat16,) if sep_only else (torch.bfloat16, torch.float32)):
+            for shared in ((False,) if sep_only else (False, True)):
                 for mode in ("philox", "replay", "p0"):
                     if dtype == torch.float32 and mode != "philox":
                         continue
