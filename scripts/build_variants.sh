@@ -24,7 +24,7 @@ for spec in "$@"; do
         for f in $srcs; do
             [ -f "$src/$f" ] || continue
             extra=""
-            [ "$f" = mcgmil.hip ] && extra="-mllvm -amdgpu-sched-strategy=max-ilp"
+            [ "$f" = mcgmil.hip ] && extra="${GATE_SCHED--mllvm -amdgpu-sched-strategy=max-ilp}"
             /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -c -fPIC -I"$inc" \
                 -Xclang -target-feature -Xclang -packed-fp32-ops $extra $defs \
                 -o "$OUT/$name.$f.o" "$src/$f" 2>&1 | grep -v packed-fp32-ops || true
