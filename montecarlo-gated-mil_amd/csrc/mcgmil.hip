@@ -4,7 +4,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <atomic>
 #include <mutex>
 #include <string>
 
@@ -12,7 +11,6 @@
 #include "mcgmil_error.h"
 #include "mcgmil_kernels.h"
 #include "mcgmil_gate_pp.h"
-#include "mcgmil_gate_hp.h"
 
 namespace mcgmil_detail {
 
@@ -172,37 +170,6 @@ int launch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_pipe_kernel launch");
 }
 
-int gate_cu_count() {
-    static std::atomic<int> cache[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
-    if (dev < 64) {
-        const int c = cache[dev].load(std::memory_order_relaxed);
-        if (c > 0) return c;
-    }
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-        cus = 256;
-    if (dev < 64) cache[dev].store(cus, std::memory_order_relaxed);
-    return cus;
-}
-
-// Separate heads in ping-pong (mcgmil_gate_hp.h): persistent, one workgroup per CU.
-int launch_gate_hp(const mcgmil::GateParams& gp, hipStream_t s) {
-    auto* k = &mcgmil::gate_hp_kernel;
-    static std::once_flag once;
-    std::call_once(once, [&] { raise_lds_cap(k); });
-    const long long tiles = (gp.total_samples + mcgmil::kHpBM - 1) / mcgmil::kHpBM;
-    if (tiles == 0) return MCGMIL_OK;
-    if (gp.uniform_rows <= 0)
-        if (int rc = launch_plan(gp, mcgmil::kHpBM, s)) return rc;
-    const long long cus = gate_cu_count();
-    const long long grid = tiles < cus ? tiles : cus;
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(mcgmil::kGateThreads), mcgmil::hp_lds_bytes(), s, gp);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_hp_kernel launch");
-}
-
 template <typename E, int RT, int PPW, int MAXC, bool REPLAY, bool ONE>
 int launch_gate_pp(const mcgmil::GateParams& gp, hipStream_t s) {
     constexpr int BM = 16 * RT;
@@ -230,7 +197,6 @@ int gate_mode() {   // 0 auto, 1 pipe, 2 pp
         const char* e = getenv("MCGMIL_GATE");
         if (e && strcmp(e, "pipe") == 0) return 1;
         if (e && strcmp(e, "pp") == 0) return 2;
-        if (e && strcmp(e, "hp") == 0) return 3;
         return MCGMIL_GATE_DEFAULT;
     }();
     return mode;
@@ -262,10 +228,6 @@ int dispatch_gate_maxc(const mcgmil::GateParams& gp, int L, int dtype, hipStream
     const bool pipe_ok = L % 64 == 0;          // the pipelined K loop is unrolled by two steps
     if constexpr (sizeof(E) == 2) {
         const int mode = gate_mode();
-        // separate heads of the reference shape (2 classes, D = 128): the two heads in ping-pong
-        if (mode == 3 && L == 32 * mcgmil::kHpKS && gp.keep_feat == nullptr && gp.keep_att == nullptr &&
-            gp.G == 2 && gp.C == 2 && gp.D == mcgmil::kHpD)
-            return launch_gate_hp(gp, s);
         if (pipe_ok && mode != 1) {
             if (gp.P <= 2 * mcgmil::kPPWaves) return dispatch_gate_pp<8, 2, MAXC>(gp, s);
             if (mode == 2 && gp.P <= 4 * mcgmil::kPPWaves) return dispatch_gate_pp<4, 4, MAXC>(gp, s);
