@@ -240,8 +240,9 @@ def main():
     traffic, traffic_src = measured_traffic(N, T, B, args.dtype, args.shared) \
         if args.workload == "cfg3" else (None, None)
     if rank == 0:
-        cpu = None if args.no_cpu_baseline else cpu_baseline(N, T, L, D, C, bool(args.shared),
-                                                             args.cpu_budget)
+        # the CPU baseline is a rank-0, N=1 figure: at N > 1 it would only hold the other ranks
+        cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(N, T, L, D, C, bool(args.shared),
+                                                                          args.cpu_budget)
         out = {
             "metric": METRIC, "value": value, "unit": "bag-samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps,

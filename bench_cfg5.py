@@ -156,7 +156,7 @@ def run(args, world, rank, dev, peak_tflops):
                  "Y_abs": float((ob["Y"] - of["Y"]).abs().max()),
                  "features_nrel": float((ob["features"].double() - of["features"].double()).abs().max()
                                         / of["features"].double().abs().max())}
-    cpu = None if args.no_cpu_baseline else cpu_baseline(k, T)
+    cpu = None if args.no_cpu_baseline or world > 1 or rank != 0 else cpu_baseline(k, T)   # rank 0, N=1
     images = world * args.steps
     return {
         "metric": "end-to-end images/sec x MCDO-samples (T=100), config 5", "value": images * T / el,
