@@ -25,8 +25,10 @@ for spec in "$@"; do
             [ -f "$src/$f" ] || continue
             extra=""
             [ "$f" = mcgmil.hip ] && extra="${GATE_SCHED--mllvm -amdgpu-sched-strategy=max-ilp}"
+            nopk="-Xclang -target-feature -Xclang -packed-fp32-ops"
+            [[ " $defs " == *" -DMCGMIL_PACKED=1 "* ]] && nopk=""   # packed-fp32 codegen on
             /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -c -fPIC -I"$inc" \
-                -Xclang -target-feature -Xclang -packed-fp32-ops $extra $defs \
+                $nopk $extra $defs \
                 -o "$OUT/$name.$f.o" "$src/$f" 2>&1 | grep -v packed-fp32-ops || true
             objs="$objs $OUT/$name.$f.o"
         done
