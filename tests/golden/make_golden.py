@@ -197,6 +197,14 @@ def dump_checkpoint_keys():
         json.dump(out, f, indent=1)
 
 
+def p1_cases():
+    """p = 1: torch's Dropout zeroes everything (the feature path becomes the gate biases alone,
+    every logit is 0 and the softmax uniform); the build's scale is 0 and its threshold 65536."""
+    run_case("edge_N50_T3_sep_p1", N=50, T=3, p_f=1.0, p_a=1.0, h_seed=31, w_seed=32, mask_seed=33)
+    run_case("edge_N40_T3_shared_pf1", N=40, T=3, shared=True, p_f=1.0, p_a=0.1, h_seed=34,
+             w_seed=35, mask_seed=36)
+
+
 def main():
     if not os.path.isdir(REF):
         raise SystemExit("make_golden.py needs the reference checkout at /root/reference")
@@ -208,6 +216,8 @@ def main():
             dump_checkpoint_keys()
         if "big" in only:
             big_cases()
+        if "p1" in only:
+            p1_cases()
         return
     dump_head_keys()
     dump_checkpoint_keys()
@@ -233,6 +243,7 @@ def main():
              mask_seed=27)
     run_case("edge_N64_T2_sep_p09", N=64, T=2, p_f=0.9, p_a=0.9, h_seed=28, w_seed=29,
              mask_seed=30)
+    p1_cases()
     # (2) config 2: N=512, T=30, fp32
     run_case("cfg2_N512_T30_sep", N=512, T=30, h_seed=42, w_seed=0, mask_seed=42, bag_ctr=0)
     run_case("cfg2_N512_T30_shared", N=512, T=30, shared=True, h_seed=42, w_seed=0,
