@@ -693,6 +693,72 @@ __global__ __launch_bounds__(256) void softmax_pool_kernel(const int32_t* bag_of
     }
     const size_t R0 = (size_t)T * ob + (size_t)t * Nb;
     const size_t abase = (size_t)T * C * ob + (size_t)t * C * Nb;
+    if (C == 2 && Nb <= 256 * kSoftmaxRows) {
+        // The reference's two classes together: one 8-byte load per row of logits and of z, and
+        // the two classes' reductions share their barriers. Per class the arithmetic and its
+        // order are the register path's below, so A and Y are bitwise the same.
+        __shared__ float sred2[4][4];
+        float e0[kSoftmaxRows], e1[kSoftmaxRows];
+        float m0 = -INFINITY, m1 = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < kSoftmaxRows; ++k) {
+            const int n = tid + 256 * k;
+            float2 l = make_float2(-INFINITY, -INFINITY);
+            if (n < Nb) l = *reinterpret_cast<const float2*>(logits + (R0 + n) * 2);
+            e0[k] = l.x;
+            e1[k] = l.y;
+            m0 = fmaxf(m0, e0[k]);
+            m1 = fmaxf(m1, e1[k]);
+        }
+        m0 = wave_max(m0);
+        m1 = wave_max(m1);
+        if (lane == 0) { sred2[0][wave] = m0; sred2[1][wave] = m1; }
+        __syncthreads();
+        m0 = fmaxf(fmaxf(sred2[0][0], sred2[0][1]), fmaxf(sred2[0][2], sred2[0][3]));
+        m1 = fmaxf(fmaxf(sred2[1][0], sred2[1][1]), fmaxf(sred2[1][2], sred2[1][3]));
+        __syncthreads();
+        float s0 = 0.f, y0 = 0.f, s1 = 0.f, y1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < kSoftmaxRows; ++k) {
+            const int n = tid + 256 * k;
+            if (n < Nb) {
+                const float2 z = *reinterpret_cast<const float2*>(zz + (R0 + n) * 2);
+                e0[k] = expf(e0[k] - m0);
+                e1[k] = expf(e1[k] - m1);
+                s0 += e0[k];
+                s1 += e1[k];
+                y0 = fmaf(e0[k], z.x, y0);
+                y1 = fmaf(e1[k], z.y, y1);
+            }
+        }
+        s0 = wave_sum(s0);
+        y0 = wave_sum(y0);
+        s1 = wave_sum(s1);
+        y1 = wave_sum(y1);
+        if (lane == 0) {
+            sred2[0][wave] = s0; sred2[1][wave] = y0; sred2[2][wave] = s1; sred2[3][wave] = y1;
+        }
+        __syncthreads();
+        s0 = (sred2[0][0] + sred2[0][1]) + (sred2[0][2] + sred2[0][3]);
+        y0 = (sred2[1][0] + sred2[1][1]) + (sred2[1][2] + sred2[1][3]);
+        s1 = (sred2[2][0] + sred2[2][1]) + (sred2[2][2] + sred2[2][3]);
+        y1 = (sred2[3][0] + sred2[3][1]) + (sred2[3][2] + sred2[3][3]);
+        const float inv0 = 1.0f / s0, inv1 = 1.0f / s1;
+        if (A) {
+            float* Ao0 = A + abase;
+            float* Ao1 = Ao0 + Nb;
+#pragma unroll
+            for (int k = 0; k < kSoftmaxRows; ++k) {
+                const int n = tid + 256 * k;
+                if (n < Nb) {
+                    Ao0[n] = e0[k] * inv0;
+                    Ao1[n] = e1[k] * inv1;
+                }
+            }
+        }
+        if (tid == 0) { Yo[0] = y0 * inv0; Yo[1] = y1 * inv1; }
+        return;
+    }
     for (int c = 0; c < C; ++c) {
         if (Nb <= 256 * kSoftmaxRows) {
             // the bag's logits of class c stay in registers: one read of logits and z, one exp
