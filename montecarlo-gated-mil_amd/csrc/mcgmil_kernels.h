@@ -154,9 +154,28 @@ constexpr float kMLog2e = -1.4426950408889634f;    // -1 / ln 2
 // rt*16 + (lane & 15) and d = 16*db + 4*(lane >> 4) + v (16x16 C layout, weights as A).
 // ONE_CLASS: every pair of this wave belongs to gate g and feeds class g only (separate
 // heads): one accumulator, part[0]. Otherwise part[c] for every class (shared gate).
+// Head vectors of one gate pair as fold_pairs uses them: bv and bu pre-scaled, wa of its class.
+struct HeadVec { f32x4 bv, bu, wa; };
+
+template <int PPW>
+__device__ __forceinline__ void load_head_vectors(const GateParams& p, int q0, int lane,
+                                                  HeadVec (&hv)[PPW]) {
+    const int DB = p.D >> 4;
+#pragma unroll
+    for (int jp = 0; jp < PPW; ++jp) {
+        const int q = q0 + jp < p.P ? q0 + jp : p.P - 1;
+        const int g = q / DB, db = q - g * DB;
+        const int d0 = db * 16 + 4 * (lane >> 4);
+        hv[jp].bv = *reinterpret_cast<const f32x4*>(p.bv + (size_t)g * p.D + d0) * kM2Log2e;
+        hv[jp].bu = *reinterpret_cast<const f32x4*>(p.bu + (size_t)g * p.D + d0) * kMLog2e;
+        hv[jp].wa = *reinterpret_cast<const f32x4*>(p.wa + (size_t)g * p.D + d0);
+    }
+}
+
 template <int RT, int PPW, int MAXC, bool ONE_CLASS>
 __device__ __forceinline__ void fold_pairs(const GateParams& p, const f32x4 (&acc)[RT][2 * PPW],
-                                           int q0, int lane, float (&part)[MAXC][RT]) {
+                                           int q0, int lane, float (&part)[MAXC][RT],
+                                           const HeadVec* pre = nullptr) {
     const int DB = p.D >> 4;
     const float av_s = p.sf * kM2Log2e, au_s = p.sf * kMLog2e;
 #pragma unroll
@@ -165,18 +184,27 @@ __device__ __forceinline__ void fold_pairs(const GateParams& p, const f32x4 (&ac
         if (q >= p.P) break;
         const int g = q / DB, db = q - g * DB;
         const int d0 = db * 16 + 4 * (lane >> 4);
-        f32x4 bvv = *reinterpret_cast<const f32x4*>(p.bv + (size_t)g * p.D + d0);
-        f32x4 buv = *reinterpret_cast<const f32x4*>(p.bu + (size_t)g * p.D + d0);
-        bvv *= kM2Log2e;
-        buv *= kMLog2e;
+        f32x4 bvv, buv;
         f32x4 coef[MAXC];
+        if (ONE_CLASS && pre) {      // loaded before the K loop (load_head_vectors)
+            bvv = pre[jp].bv;
+            buv = pre[jp].bu;
+            coef[0] = pre[jp].wa;
 #pragma unroll
-        for (int c = 0; c < MAXC; ++c) {
-            const int cc = ONE_CLASS ? g : c;
-            const bool use = ONE_CLASS ? (c == 0) : ((c < p.C) && (p.G == 1 || c == g));
-            // address stays inside wa[C, D] for every c; unused classes get 0
-            const f32x4 w = *reinterpret_cast<const f32x4*>(p.wa + (size_t)(use ? cc : 0) * p.D + d0);
-            coef[c] = use ? w : f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int c = 1; c < MAXC; ++c) coef[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
+            bvv = *reinterpret_cast<const f32x4*>(p.bv + (size_t)g * p.D + d0);
+            buv = *reinterpret_cast<const f32x4*>(p.bu + (size_t)g * p.D + d0);
+            bvv *= kM2Log2e;
+            buv *= kMLog2e;
+#pragma unroll
+            for (int c = 0; c < MAXC; ++c) {
+                const int cc = ONE_CLASS ? g : c;
+                const bool use = ONE_CLASS ? (c == 0) : ((c < p.C) && (p.G == 1 || c == g));
+                // address stays inside wa[C, D] for every c; unused classes get 0
+                const f32x4 w = *reinterpret_cast<const f32x4*>(p.wa + (size_t)(use ? cc : 0) * p.D + d0);
+                coef[c] = use ? w : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
         }
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
@@ -512,6 +540,12 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     __syncthreads();
     MCGMIL_STAMP(p, 2);
 
+    // bf16 separate heads: the epilogue's head vectors load under the K loop instead of after it
+    // (+0.3-1.4% in same-process A/B, bitwise equal; profiles/r02/gate_ab.log). The fp32 kernel
+    // has no registers to spare for them.
+    constexpr bool kEarlyHV = ONE_CLASS && sizeof(E) == 2;
+    HeadVec hvec[PPW];
+    if constexpr (kEarlyHV) load_head_vectors<PPW>(p, q0, lane, hvec);
     // KS is even and >= 2 (host guarantees L % 64 == 0). The first two steps are peeled: their
     // MFMAs take the zero accumulators as an inline-constant C operand, so no register copies of
     // the 132 zeroed accumulators are made on the way into the loop.
@@ -531,7 +565,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     for (int c = 0; c < MAXC; ++c)
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) part[c][rt] = 0.f;
-    fold_pairs<RT, PPW, MAXC, ONE_CLASS>(p, acc, q0, lane, part);
+    fold_pairs<RT, PPW, MAXC, ONE_CLASS>(p, acc, q0, lane, part, kEarlyHV ? hvec : nullptr);
     MCGMIL_STAMP(p, 4);
     // ONE_CLASS: the wave's pairs all belong to gate q0 / (D/16) (idle waves: class >= C)
     const int one_class = ONE_CLASS ? (q0 < p.P ? q0 / (p.D >> 4) : MAXC) : -1;
