@@ -149,11 +149,6 @@ __device__ __forceinline__ float gated_product_scaled(float ax, float by) {
 constexpr float kM2Log2e = -2.8853900817779268f;   // -2 / ln 2
 constexpr float kMLog2e = -1.4426950408889634f;    // -1 / ln 2
 
-// Fold the gate pairs of one pass into per-lane partial scores. acc[rt][2j] / acc[rt][2j+1]
-// hold V / U pre-activations (before the dropout scale) of pair q0 + j for instance
-// rt*16 + (lane & 15) and d = 16*db + 4*(lane >> 4) + v (16x16 C layout, weights as A).
-// ONE_CLASS: every pair of this wave belongs to gate g and feeds class g only (separate
-// heads): one accumulator, part[0]. Otherwise part[c] for every class (shared gate).
 // Head vectors of one gate pair as fold_pairs uses them: bv and bu pre-scaled, wa of its class.
 struct HeadVec { f32x4 bv, bu, wa; };
 
@@ -172,6 +167,11 @@ __device__ __forceinline__ void load_head_vectors(const GateParams& p, int q0, i
     }
 }
 
+// Fold the gate pairs of one pass into per-lane partial scores. acc[rt][2j] / acc[rt][2j+1]
+// hold V / U pre-activations (before the dropout scale) of pair q0 + j for instance
+// rt*16 + (lane & 15) and d = 16*db + 4*(lane >> 4) + v (16x16 C layout, weights as A).
+// ONE_CLASS: every pair of this wave belongs to gate g and feeds class g only (separate
+// heads): one accumulator, part[0]. Otherwise part[c] for every class (shared gate).
 template <int RT, int PPW, int MAXC, bool ONE_CLASS>
 __device__ __forceinline__ void fold_pairs(const GateParams& p, const f32x4 (&acc)[RT][2 * PPW],
                                            int q0, int lane, float (&part)[MAXC][RT],
