@@ -102,12 +102,28 @@ def cpu_baseline(N, T, L, D, C, shared, budget_s):
                       f"{el * 1e3 / n:.1f} ms/bag; 1 thread: {n1} bags, {el1 * 1e3 / n1:.1f} ms/bag"}
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` outside a launcher: start N rank processes through torch.distributed.run
+    (one per GPU, backend nccl = RCCL) and return their exit code. Runs before this process
+    touches the GPU, and starts the ranks as children (no exec)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)]
+    return subprocess.call(cmd + sys.argv[1:])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--bags", type=int, default=16, help="bags per GPU per step")
+    # 512 bags of N=2048 per GPU per step: ~57 ms of kernels, so the driver's 20 timed steps
+    # span > 1 s (a 16-bag step is 1.8 ms; the workload per bag is the same)
+    ap.add_argument("--bags", type=int, default=512, help="bags per GPU per step")
     ap.add_argument("--n", type=int, default=2048)
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
@@ -124,6 +140,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            return spawn_ranks(args.gpus)
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE="
+              f"{os.environ['WORLD_SIZE']} ranks", file=sys.stderr)
+        return 2
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -139,7 +162,7 @@ def main():
             print(json.dumps(out))
         if world > 1:
             dist.destroy_process_group()
-        return
+        return 0
 
     from mcgmil import _lib, ops
     from mcgmil import synthetic
@@ -271,7 +294,8 @@ def main():
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -29,6 +29,9 @@ import torch
 import torch.distributed as dist
 
 RESNET18_GFLOP = 3.64          # per 3 x 224 x 224 instance (2 x 1.82 GMAC)
+# MI355X fp32 peak, vector = matrix (no xf32 on gfx950): 157.3 TFLOP/s spec, MI355X_MICROARCH.md
+# spec table. The fp32 line's dominant stage is torch/MIOpen's fp32 layers, not this build's.
+PEAK_FP32_TFLOPS = 157.3
 H_IMG, W_IMG, PS, OVERLAP, THRESH = 7036, 2800, 224, 0.75, 0.75   # config.yml:31,34
 BLOB = (0.30, 0.58)     # semi-axes of the breast region (fractions of H, W): k = 1,507 tiles kept
 
@@ -174,11 +177,11 @@ def run(args, world, rank, dev, peak_tflops):
                    "drift_vs_fp32_pipeline": drift,
                    "stage_ms": stage_ms, "parallelism": f"one image per GPU per step, {world} GPU(s)"},
         "roofline": {"bound": "mfma", "achieved": feat_tflops,
-                     "peak": peak_tflops if bf16 else 157.3, "unit": "TFLOP/s",
-                     "frac": feat_tflops / (peak_tflops if bf16 else 157.3), "traffic": None,
+                     "peak": peak_tflops if bf16 else PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                     "frac": feat_tflops / (peak_tflops if bf16 else PEAK_FP32_TFLOPS), "traffic": None,
                      "kernel": "ResNet-18 feature extractor (the dominant stage): " +
                                ("stem + implicit-GEMM convolutions + fused BN (HIP, bf16)" if bf16 else
-                                "torch/MIOpen fp32 layers"),
+                                "torch/MIOpen fp32 layers (PyTorch-ROCm, not this build's kernels)"),
                      "algorithmic_tflop_per_launch": k * RESNET18_GFLOP / 1e3},
         "cpu_baseline": cpu,
     }

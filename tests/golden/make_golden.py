@@ -198,8 +198,11 @@ def dump_checkpoint_keys():
 
 
 def p1_cases():
-    """p = 1: torch's Dropout zeroes everything (the feature path becomes the gate biases alone,
-    every logit is 0 and the softmax uniform); the build's scale is 0 and its threshold 65536."""
+    """p_feat = 1: torch's Dropout zeroes every feature, so the gates see their biases alone and
+    every logit of a class is the same constant wa_c . (tanh(bv) * sigmoid(bu)) + ba_c; the pooled
+    embedding is 0 and Y equals the classifier bias. The attention is uniform only where p_att = 1
+    as well (edge_N50_T3_sep_p1): with p_att = 0.1 (edge_N40_T3_shared_pf1) some of those constant
+    logits are dropped to 0 and A is not uniform. The build's scale is 0, its threshold 65536."""
     run_case("edge_N50_T3_sep_p1", N=50, T=3, p_f=1.0, p_a=1.0, h_seed=31, w_seed=32, mask_seed=33)
     run_case("edge_N40_T3_shared_pf1", N=40, T=3, shared=True, p_f=1.0, p_a=0.1, h_seed=34,
              w_seed=35, mask_seed=36)

@@ -30,7 +30,12 @@ def device_asm(tmp_path_factory):
     cmd = [HIPCC, f"--offload-arch={_build.ARCH}", "-O3", "-std=c++17", f"-I{_build.INCLUDE}",
            "--cuda-device-only", "-S", "-o", out] + _build.DEVICE_FLAGS + \
         _build.SOURCE_FLAGS.get("mcgmil.hip", []) + [os.path.join(_build.CSRC, "mcgmil.hip")]
-    subprocess.run(cmd, check=True, capture_output=True)
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    except subprocess.TimeoutExpired:
+        pytest.fail("hipcc -S of mcgmil.hip took more than 900 s")
+    if r.returncode != 0:
+        pytest.fail(f"hipcc -S of mcgmil.hip failed ({r.returncode}):\n{r.stderr[-4000:]}")
     with open(out) as f:
         text = f.read()
     shutil.rmtree(os.path.dirname(out), ignore_errors=True)

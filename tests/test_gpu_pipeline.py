@@ -114,3 +114,46 @@ def test_mc_predict_image_bf16_features(cuda):
     print(f"bf16-vs-fp32 pipeline drift: prob_mean {dp:.3g}, A_mean nrel {am:.3g}, Y {dy:.3g}")
     assert dp < DRIFT_PROB_MEAN and am < DRIFT_A_MEAN and dy < DRIFT_Y
     assert torch.isfinite(b["att_mean"]).all() and torch.isfinite(b["att_std"]).all()
+
+
+# BASELINE config 5 itself (bench.py --workload cfg5: the 7036 x 2800 synthetic mammogram, 224-px
+# tiles at overlap 0.75 / empty_thresh 0.75, k = 1,507 instances, T = 100, the bench's model and
+# seed): the bf16 pipeline's uncertainty outputs against the fp32 pipeline's. Measured in round 2
+# (profiles/r02/bench_cfg5_bf16.log): A_mean nrel 9.9e-3, A_var nrel 4.1e-2, prob_mean 3.2e-5,
+# Y 7.2e-4, features nrel 2.8e-2. The bounds are 1.5x those. The drift enters in the backbone
+# (the bf16 ResNet moves the features by ~3% before the head; the bf16 head alone adds ~5e-3 to
+# A_mean, tests/test_gpu_parity.py::test_bf16_drift_vs_fp32_reference).
+CFG5_DRIFT = dict(A_mean=1.5 * 9.9e-3, A_var=1.5 * 4.1e-2, prob_mean=1.5 * 3.2e-5, Y=1.5 * 7.2e-4)
+
+
+def test_cfg5_bf16_uncertainty_drift(cuda):
+    import bench_cfg5 as C5
+    from mcgmil import MultiHeadGatedAttentionMIL, deactivate_batchnorm
+    from mcgmil.infer import mc_predict_image
+    from mcgmil.patcher import ImagePatcher
+    torch.manual_seed(0)                                  # bench_cfg5.run's model
+    model = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=False)
+    model.apply(deactivate_batchnorm)
+    model.to(cuda).eval()
+    model.feature_extractor.to(memory_format=torch.channels_last)
+    patcher = ImagePatcher(patch_size=C5.PS, overlap=C5.OVERLAP, empty_thresh=C5.THRESH)
+    patcher.get_tiles(C5.H_IMG, C5.W_IMG)
+    img = C5.synthetic_mammogram(cuda, seed=5)
+    seed = 6                                              # the bench's drift image (warmup 2, steps 5)
+    model.compute_dtype = torch.bfloat16
+    b = mc_predict_image(model, patcher, img, T=100, seed=seed, features_dtype=torch.bfloat16)
+    model.compute_dtype = torch.float32
+    a = mc_predict_image(model, patcher, img, T=100, seed=seed, features_dtype=None)
+    assert len(a["tiles_indices"]) == 1507
+    assert np.array_equal(a["tiles_indices"], b["tiles_indices"])
+
+    def nr(k):
+        x, y = b[k].double(), a[k].double()
+        return float((x - y).abs().max() / y.abs().max())
+
+    d = dict(A_mean=nr("A_mean"), A_var=nr("A_var"),
+             prob_mean=float((a["prob_mean"] - b["prob_mean"]).abs().max()),
+             Y=float((a["Y"] - b["Y"]).abs().max()), features=nr("features"))
+    print("config-5 bf16-vs-fp32 drift: " + ", ".join(f"{k} {v:.3g}" for k, v in d.items()))
+    for k, bound in CFG5_DRIFT.items():
+        assert d[k] <= bound, (k, d[k], bound)
