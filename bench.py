@@ -3,12 +3,13 @@
 Metric (BASELINE.json): bags/sec x MCDO-samples (T=100) at N=2048, d=512 -- BASELINE config 3
 (N=2048 instances/bag, L=d=512, D=128, C=2 heads, separate attention as config.yml:8, T=100,
 bf16 operands, fp32 accumulate / softmax / outputs). A step = one pass of the hot path over one
-batch of --bags synthetic bags per GPU already resident in HBM: gate-score kernel (all T
-samples, Philox masks in-register) + softmax/pooling + per-bag attention mean/var, and for
-N > 1 GPUs the gather of the per-bag predictions Y[T, C] to every rank (weak scaling: every
-rank owns --bags bags).
+batch of --bags synthetic bags per GPU already resident in HBM: ONE launch of gate_fused_kernel
+(all T samples' gate scores with in-register Philox masks, softmax over instances and attention
+pooling; the two-kernel path gate_pipe_kernel + softmax_pool_kernel for batches too small to
+fill the GPU region by region) + per-bag attention mean/var, and for N > 1 GPUs the gather of
+the per-bag predictions Y[T, C] to every rank (weak scaling: every rank owns --bags bags).
 
-Prints ONE JSON line (rank 0). `roofline` prices the dominant kernel (gate_scores) with the
+Prints ONE JSON line (rank 0). `roofline` prices the dominant kernel (the gate kernel) with the
 ALGORITHMIC FLOPs of the literal reference computation against the bf16 dense
 MFMA peak; its time comes from HIP events around that kernel on the launch stream.
 `cpu_baseline` times the reference op sequence (oracle/mcdo_ref.py, torch CPU, with its own
@@ -221,13 +222,23 @@ def main():
     else:
         gather = None
 
+    # ONE launch (gate_fused_kernel: gate scores + softmax + pooling) when the batch is large
+    # enough, else gate_pipe_kernel + softmax_pool_kernel; the events bracket the gate kernel
+    regions = ctypes.c_int64()
+    _lib.check(lib.mcgmil_fused_regions(pa, ctypes.byref(regions)), "fused_regions")
+    fused = regions.value > 0
+
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        _lib.check(lib.mcgmil_gate_scores(pa, sh), "gate_scores")
+        if fused:
+            _lib.check(lib.mcgmil_gate_softmax_pool(pa, sh), "gate_softmax_pool")
+        else:
+            _lib.check(lib.mcgmil_gate_scores(pa, sh), "gate_scores")
         if ev is not None:
             ev[1].record(stream)
-        _lib.check(lib.mcgmil_softmax_pool(pa, sh), "softmax_pool")
+        if not fused:
+            _lib.check(lib.mcgmil_softmax_pool(pa, sh), "softmax_pool")
         _lib.check(lib.mcgmil_bag_stats(pa, sh), "bag_stats")
         if gather is not None:       # per-bag predictions to every rank (RCCL over xGMI)
             Ypad[:B].copy_(Y)
@@ -284,7 +295,9 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[args.dtype],
                          "unit": "TFLOP/s", "frac": achieved / PEAK_TFLOPS[args.dtype],
                          "traffic": traffic, "traffic_unit": "HBM bytes per launch",
-                         "traffic_source": traffic_src, "kernel": "gate_pipe_kernel",
+                         "traffic_source": traffic_src,
+                         "kernel": (f"gate_fused_kernel (gate scores + softmax + pooling, one launch, "
+                                    f"{regions.value} regions)" if fused else "gate_pipe_kernel"),
                          "kernel_ms": gate_ms, "algorithmic_tflop_per_launch": F / 1e12},
             "roofline_hbm": {"achieved": hbm_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": hbm_gbs / PEAK_HBM_GBS,

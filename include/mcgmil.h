@@ -18,8 +18,11 @@
  *                              net_utils.py:207-208) when A_mean/A_var/P_mean are requested
  *   mcgmil_pack_weights   <- the parameter layout of __init__ (model.py:182-203), re-laid out
  *                            for the kernel once per model
+ *   mcgmil_gate_softmax_pool
+ *                         <- model.py:280-316 for all T samples: the two stages below, or ONE
+ *                            fused launch (MCGMIL_FUSED); A and Y are bitwise the same either way
  *   mcgmil_gate_scores / mcgmil_softmax_pool / mcgmil_bag_stats
- *                         <- the three stages of mcgmil_mcdo_forward, exposed for profiling
+ *                         <- the stages of mcgmil_mcdo_forward, exposed for profiling
  *   mcgmil_feature_keep / mcgmil_attention_keep
  *                         <- the dropout masks the kernel draws (nn.Dropout at model.py:206-209),
  *                            materialised for parity tests
@@ -118,10 +121,19 @@ int mcgmil_packed_weights_size(const mcgmil_args* a, size_t* bytes);
 /* Re-lay the fp32 parameters out as MFMA operand tiles of dtype h_dtype into `packed`. */
 int mcgmil_pack_weights(const mcgmil_args* a, void* packed, void* stream);
 
-/* The whole hot path: [pack] -> gate scores -> softmax + pooling -> [statistics]. */
+/* The whole hot path: [pack] -> gate scores + softmax + pooling -> [statistics]. */
 int mcgmil_mcdo_forward(const mcgmil_args* a, void* stream);
 
-/* Its stages (same args/workspace; call in this order, after packing if packed_w is NULL). */
+/* Its stages (same args/workspace; call in this order, after packing if packed_w is NULL):
+ * mcgmil_gate_softmax_pool, then mcgmil_bag_stats. mcgmil_gate_softmax_pool is
+ * mcgmil_gate_scores followed by mcgmil_softmax_pool, or ONE fused launch when the environment
+ * asks for it: MCGMIL_FUSED=1 (whenever it applies) or MCGMIL_FUSED=auto (batches of >= 16,384
+ * regions). Both give bitwise the same A and Y. */
+int mcgmil_gate_softmax_pool(const mcgmil_args* a, void* stream);
+/* The fused launch mcgmil_gate_softmax_pool would make for these args: *regions = its number of
+ * workgroups (one per region of t-groups of a bag; an upper bound for ragged bags), or 0 when
+ * it would run the two-kernel path. Launches nothing. */
+int mcgmil_fused_regions(const mcgmil_args* a, int64_t* regions);
 int mcgmil_gate_scores(const mcgmil_args* a, void* stream);
 int mcgmil_softmax_pool(const mcgmil_args* a, void* stream);
 int mcgmil_bag_stats(const mcgmil_args* a, void* stream);

@@ -11,6 +11,7 @@
 #include "mcgmil_error.h"
 #include "mcgmil_kernels.h"
 #include "mcgmil_gate_pp.h"
+#include "mcgmil_fused.h"
 
 namespace mcgmil_detail {
 
@@ -89,7 +90,7 @@ int validate_batch(const mcgmil_args* a) {
 
 struct Layout {
     size_t packed_bytes;   // 0 when args->packed_w is supplied
-    size_t logits_off, zz_off, plan_off, total;
+    size_t logits_off, zz_off, plan_off, region_off, total;
 };
 
 // Smallest row tile any gate kernel uses (sizes the tile plan).
@@ -108,7 +109,8 @@ Layout layout_for(const mcgmil_args* a) {
     l.zz_off = l.logits_off + scores;
     l.plan_off = l.zz_off + scores;
     const size_t max_tiles = ((size_t)a->T * a->total_rows + kMinBM - 1) / kMinBM;
-    l.total = l.plan_off + align_up(max_tiles * sizeof(int32_t), 256);
+    l.region_off = l.plan_off + align_up(max_tiles * sizeof(int32_t), 256);
+    l.total = l.region_off + align_up(((size_t)a->num_bags + 1) * sizeof(int32_t), 256);
     return l;
 }
 
@@ -247,6 +249,58 @@ int dispatch_gate(const mcgmil::GateParams& gp, int L, int dtype, hipStream_t s)
                      : dispatch_gate_maxc<E, 4>(gp, L, dtype, s);
 }
 
+// Fused single launch (gate_fused_kernel) or the two-kernel path (gate scores into the
+// workspace, then softmax_pool_kernel)? The fused kernel runs the pipelined gate kernel's tiles
+// (Philox masks, no replay); a workgroup owns a whole region (~32 tiles at config 3), so it
+// needs many regions to fill 256 CUs without a tail: MCGMIL_FUSED=auto takes it for batches of
+// >= 16,384 regions (64 per CU), MCGMIL_FUSED=1 whenever it applies. By default (unset or 0) the
+// two-kernel path runs: on MI355X the fused kernel measured 11-19% slower at config 3 (same
+// tiles, bitwise the same outputs), against ~1% for the softmax launch it saves.
+constexpr long long kFusedMinRegions = 16384;
+
+int fused_mode() {   // -1 auto, 0 off, 1 on (read per call: tests switch it in one process)
+    const char* e = getenv("MCGMIL_FUSED");
+    if (e && strcmp(e, "1") == 0) return 1;
+    if (e && strcmp(e, "auto") == 0) return -1;
+    return 0;       // default: the two-kernel path (measured faster, DESIGN.md §4 gate_fused_kernel)
+}
+
+// Returns 1 if the fused kernel was launched (with `regions` set: nothing is launched, *regions
+// = its grid), 0 if the caller must run the two-kernel path.
+template <typename E, int MAXC>
+int try_fused_maxc(const mcgmil::GateParams& gp, long long total_rows, int L, hipStream_t s, int* rc,
+                   long long* regions = nullptr) {
+    *rc = MCGMIL_OK;
+    // (L >= 128: the fused pipeline peels two K steps at each end of a tile)
+    if (gp.keep_feat || L % 64 != 0 || L < 128 || gp.P > 2 * mcgmil::kGateWaves) return 0;
+    if constexpr (sizeof(E) == 2) {       // bf16: the kernel dispatch_gate_maxc would pick
+        const int mode = gate_mode();
+        const bool pipe = mode == 1 || (mode == 0 && gp.P > 2 * mcgmil::kPPWaves);
+        if (!pipe) return 0;
+    }
+    const int fm = fused_mode();
+    if (fm == 0) return 0;
+    if (fm < 0 && mcgmil_detail::fused_regions(gp, total_rows, mcgmil::fused_cap<MAXC>(), true) <
+                      kFusedMinRegions)
+        return 0;
+    // same kernel shape as dispatch_gate_pipe: one class per wave for separate heads
+    const int ppw = gp.P <= mcgmil::kGateWaves ? 1 : 2;
+    const bool one = gp.G > 1 && gp.G == gp.C && (gp.D / 16) % ppw == 0;
+    if (regions) {
+        *regions = mcgmil_detail::fused_regions(gp, total_rows, mcgmil::fused_cap<MAXC>(), false);
+        return 1;
+    }
+    *rc = mcgmil_detail::launch_gate_fused(gp, sizeof(E) == 2, ppw, MAXC, one, total_rows, s);
+    return 1;
+}
+
+template <typename E>
+int try_fused(const mcgmil::GateParams& gp, long long total_rows, int L, hipStream_t s, int* rc,
+              long long* regions = nullptr) {
+    return gp.C <= 2 ? try_fused_maxc<E, 2>(gp, total_rows, L, s, rc, regions)
+                     : try_fused_maxc<E, 4>(gp, total_rows, L, s, rc, regions);
+}
+
 }  // namespace
 
 extern "C" {
@@ -291,7 +345,13 @@ int mcgmil_pack_weights(const mcgmil_args* a, void* packed, void* stream) {
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "pack_weights_kernel launch");
 }
 
-int mcgmil_gate_scores(const mcgmil_args* a, void* stream) {
+}  // extern "C"
+
+namespace {
+
+// Validation of the gate kernels' inputs and their launch parameters (mcgmil_gate_scores,
+// mcgmil_gate_softmax_pool).
+int gate_params(const mcgmil_args* a, mcgmil::GateParams& gp) {
     int rc = validate_batch(a);
     if (rc) return rc;
     const Layout l = layout_for(a);
@@ -307,7 +367,6 @@ int mcgmil_gate_scores(const mcgmil_args* a, void* stream) {
         return fail(MCGMIL_E_INVALID, "replay mode needs both keep_feat and keep_att");
     if (a->packed_w && !aligned16(a->packed_w)) return fail(MCGMIL_E_ALIGN, "packed_w must be 16-byte aligned");
 
-    mcgmil::GateParams gp;
     gp.H = a->H;
     gp.ldh = a->ldh;
     gp.bag_off = a->bag_offsets;
@@ -342,10 +401,51 @@ int mcgmil_gate_scores(const mcgmil_args* a, void* stream) {
     gp.stamps = static_cast<unsigned long long*>(a->debug);
     gp.tile_bag = reinterpret_cast<const int32_t*>(static_cast<char*>(a->workspace) + l.plan_off);
     gp.uniform_rows = a->uniform_bag_rows;
+    gp.Y = a->Y;
+    gp.A = a->A;
+    gp.region_off = reinterpret_cast<const int32_t*>(static_cast<char*>(a->workspace) + l.region_off);
+    gp.region_t = a->uniform_bag_rows > 0
+                      ? mcgmil::region_t_groups(a->uniform_bag_rows, a->T,
+                                                a->C <= 2 ? mcgmil::fused_cap<2>() : mcgmil::fused_cap<4>())
+                      : 0;
+    return MCGMIL_OK;
+}
 
+}  // namespace
+
+extern "C" {
+
+int mcgmil_gate_scores(const mcgmil_args* a, void* stream) {
+    mcgmil::GateParams gp;
+    if (int rc = gate_params(a, gp)) return rc;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (a->h_dtype == MCGMIL_BF16) return dispatch_gate<__bf16>(gp, a->L, a->h_dtype, s);
     return dispatch_gate<float>(gp, a->L, a->h_dtype, s);
+}
+
+int mcgmil_fused_regions(const mcgmil_args* a, int64_t* regions) {
+    if (!regions) return fail(MCGMIL_E_INVALID, "regions is NULL");
+    mcgmil::GateParams gp;
+    if (int rc = gate_params(a, gp)) return rc;
+    int rc = MCGMIL_OK;
+    long long r = 0;
+    const int fused = a->h_dtype == MCGMIL_BF16 ? try_fused<__bf16>(gp, a->total_rows, a->L, nullptr, &rc, &r)
+                                                : try_fused<float>(gp, a->total_rows, a->L, nullptr, &rc, &r);
+    *regions = fused ? r : 0;
+    return MCGMIL_OK;
+}
+
+int mcgmil_gate_softmax_pool(const mcgmil_args* a, void* stream) {
+    mcgmil::GateParams gp;
+    if (int rc = gate_params(a, gp)) return rc;
+    if (!a->Y) return fail(MCGMIL_E_INVALID, "Y is NULL");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc = MCGMIL_OK;
+    const int fused = a->h_dtype == MCGMIL_BF16 ? try_fused<__bf16>(gp, a->total_rows, a->L, s, &rc)
+                                                : try_fused<float>(gp, a->total_rows, a->L, s, &rc);
+    if (fused) return rc;
+    if ((rc = mcgmil_gate_scores(a, stream))) return rc;
+    return mcgmil_softmax_pool(a, stream);
 }
 
 int mcgmil_softmax_pool(const mcgmil_args* a, void* stream) {
@@ -389,8 +489,7 @@ int mcgmil_mcdo_forward(const mcgmil_args* a, void* stream) {
     if (!a->packed_w) {
         if ((rc = mcgmil_pack_weights(a, a->workspace, stream))) return rc;
     }
-    if ((rc = mcgmil_gate_scores(a, stream))) return rc;
-    if ((rc = mcgmil_softmax_pool(a, stream))) return rc;
+    if ((rc = mcgmil_gate_softmax_pool(a, stream))) return rc;
     return mcgmil_bag_stats(a, stream);
 }
 

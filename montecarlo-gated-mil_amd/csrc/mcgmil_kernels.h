@@ -43,6 +43,11 @@ struct GateParams {
     const uint8_t* keep_att;
     float* logits;                 // [T*total_rows, C]
     float* zz;                     // [T*total_rows, C]
+    // fused kernel (gate_fused_kernel) only: its outputs and its region table
+    float* Y;                      // [B, T, C]
+    float* A;                      // per bag [T, C, N_b], or nullptr
+    const int32_t* region_off;     // [B+1] prefix of per-bag region counts (ragged bags) or nullptr
+    int region_t;                  // t-groups per region when every bag has uniform_rows rows
     unsigned long long* stamps;    // diagnostic build only: [tiles][8] s_memtime stamps
 };
 
@@ -121,6 +126,7 @@ __device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0
 }
 
 // Tile plan: bag of the first row of every BM-row tile (one thread per tile).
+#ifndef MCGMIL_KERNELS_TEMPLATES_ONLY
 __global__ void plan_tiles_kernel(const int32_t* bag_off, int B, int T, long long total_samples,
                                   int BM, long long tiles, int32_t* tile_bag) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -128,6 +134,7 @@ __global__ void plan_tiles_kernel(const int32_t* bag_off, int B, int T, long lon
     const long long R = i * BM;
     tile_bag[i] = R < total_samples ? find_bag(bag_off, B, T, R) : 0;
 }
+#endif
 
 // tanh(x) * sigmoid(y) (reference model.py:183-184 / 287) evaluated as (1-a) / ((1+a)(1+b)),
 // a = e^{-2x} = 2^{ax}, b = e^{-y} = 2^{by}, from the pre-scaled arguments
@@ -253,7 +260,8 @@ __device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
                                               float (&part)[MAXC][BM / ROWS], f32x4 zacc,
                                               bool zwave, float* red, float* zred,
                                               const int* rinfo, int one_class, int waves_per_gate,
-                                              bool have_keep, bool keep) {
+                                              bool have_keep, bool keep, float* lg_out,
+                                              float* z_out, long long obase) {
     constexpr int RT = BM / ROWS;
     constexpr int NG = 64 / ROWS;                  // lane groups per accumulator tile
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -297,10 +305,232 @@ __device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
         keep = attention_keep(p.k0, p.k1, (uint32_t)ri[5], (uint32_t)(p.t_base + t), (uint32_t)c,
                               (uint32_t)n, p.thr_a);
     }
-    const size_t o = (size_t)(R0 + r) * p.C + c;
-    p.logits[o] = s * (keep ? p.sa : 0.f);
-    p.zz[o] = zred[c * BM + r] * p.sf;
+    // row R0 + r of the flattened (bag, t, n) space -> lg_out / z_out row R0 + r - obase
+    const size_t o = (size_t)(R0 + r - obase) * p.C + c;
+    lg_out[o] = s * (keep ? p.sa : 0.f);
+    z_out[o] = zred[c * BM + r] * p.sf;
 }
+
+// finish_scores for the fused pipeline: the thread's output item (row wave*16 + (lane & 15),
+// class lane >> 4) takes its row from registers (valid, sample counter tc, instance n, bag
+// counter cb) instead of the LDS row table. Same reductions, same arithmetic.
+template <int BM, int MAXC>
+__device__ __forceinline__ void score_rows(const GateParams& p, long long R0, float (&part)[MAXC][BM / 16],
+                                           f32x4 zacc, float* red, float* zred, int one_class,
+                                           int waves_per_gate, bool valid, uint32_t tc, uint32_t n,
+                                           uint32_t cb, float* lg_out, float* z_out, long long obase) {
+    constexpr int RT = BM / 16;
+    constexpr int NG = 4;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ncls = one_class < 0 ? MAXC : 1;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        if (c >= ncls) break;
+        const int cls = one_class < 0 ? c : one_class;
+        if (cls >= MAXC) break;
+        float* dst = red + ((size_t)(wave * MAXC + cls) * NG + lane / 16) * BM + (lane % 16);
+#pragma unroll
+        for (int q = 0; q < RT; ++q) dst[16 * q] = part[c][q];
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) zred[c * BM + wave * 16 + lane] = zacc[c];
+    }
+    __syncthreads();
+    const int r = wave * 16 + (lane & 15), c = lane >> 4;
+    if (r >= BM || c >= p.C || !valid) return;
+    float s = 0.f;
+    const int nw = waves_per_gate ? waves_per_gate : kGateWaves;
+    for (int k = 0; k < nw; ++k) {
+        const int w = waves_per_gate ? c * waves_per_gate + k : k;
+        const float* src = red + (size_t)(w * MAXC + c) * NG * BM + r;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) s += src[g * BM];
+    }
+    s += p.ba[c];
+    const bool keep = attention_keep(p.k0, p.k1, cb, tc, (uint32_t)c, n, p.thr_a);
+    const size_t o = (size_t)(R0 + r - obase) * p.C + c;
+    lg_out[o] = s * (keep ? p.sa : 0.f);
+    z_out[o] = zred[c * BM + r] * p.sf;
+}
+
+// ---------------------------------------------------------------------------------------
+// softmax_group: one (bag, t) group's softmax over the bag's instances (model.py:305) and
+// Y_c = sum_n A z_c (model.py:308-316), by 256 threads (ltid 0..255, 4 waves). lg / zz: the
+// group's logits and classifier projections, row-major [Nb][C] (the global workspace, or LDS
+// in the fused kernel); Ao: the group's A [C][Nb] (or nullptr); Yo: its Y[C]; sred: 16 floats of
+// LDS for this group's waves. Every caller runs this same code, so A and Y are bitwise the
+// same whichever kernel computes them. `active` = false executes only the barriers (the idle half
+// of a 512-thread workgroup); both halves of a workgroup must pass the same Nb and C.
+// ---------------------------------------------------------------------------------------
+constexpr int kSoftmaxRows = 16;    // register path for bags of up to 4096 instances
+
+__device__ __forceinline__ void softmax_group(int ltid, bool active, int Nb, int C, const float* lg,
+                                              const float* zz, float* Ao, float* Yo, float* sred) {
+    const int tid = ltid, lane = ltid & 63, wave = ltid >> 6;
+    if (Nb == 0) {
+        if (active && tid < C) Yo[tid] = 0.f;
+        return;
+    }
+    const int Nl = active ? Nb : 0;                 // rows this thread may touch
+    if (C == 2 && Nb <= 256 * kSoftmaxRows) {
+        // The reference's two classes together: one 8-byte load per row of logits and of z, and
+        // the two classes' reductions share their barriers. Per class the arithmetic and its
+        // order are the register path's below, so A and Y are bitwise the same.
+        float (*sred2)[4] = reinterpret_cast<float (*)[4]>(sred);
+        float e0[kSoftmaxRows], e1[kSoftmaxRows];
+        float m0 = -INFINITY, m1 = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < kSoftmaxRows; ++k) {
+            const int n = tid + 256 * k;
+            float2 l = make_float2(-INFINITY, -INFINITY);
+            if (n < Nl) l = *reinterpret_cast<const float2*>(lg + (size_t)n * 2);
+            e0[k] = l.x;
+            e1[k] = l.y;
+            m0 = fmaxf(m0, e0[k]);
+            m1 = fmaxf(m1, e1[k]);
+        }
+        m0 = wave_max(m0);
+        m1 = wave_max(m1);
+        if (lane == 0) { sred2[0][wave] = m0; sred2[1][wave] = m1; }
+        __syncthreads();
+        m0 = fmaxf(fmaxf(sred2[0][0], sred2[0][1]), fmaxf(sred2[0][2], sred2[0][3]));
+        m1 = fmaxf(fmaxf(sred2[1][0], sred2[1][1]), fmaxf(sred2[1][2], sred2[1][3]));
+        __syncthreads();
+        float s0 = 0.f, y0 = 0.f, s1 = 0.f, y1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < kSoftmaxRows; ++k) {
+            const int n = tid + 256 * k;
+            if (n < Nl) {
+                const float2 z = *reinterpret_cast<const float2*>(zz + (size_t)n * 2);
+                e0[k] = expf(e0[k] - m0);
+                e1[k] = expf(e1[k] - m1);
+                s0 += e0[k];
+                s1 += e1[k];
+                y0 = fmaf(e0[k], z.x, y0);
+                y1 = fmaf(e1[k], z.y, y1);
+            }
+        }
+        s0 = wave_sum(s0);
+        y0 = wave_sum(y0);
+        s1 = wave_sum(s1);
+        y1 = wave_sum(y1);
+        if (lane == 0) {
+            sred2[0][wave] = s0; sred2[1][wave] = y0; sred2[2][wave] = s1; sred2[3][wave] = y1;
+        }
+        __syncthreads();
+        s0 = (sred2[0][0] + sred2[0][1]) + (sred2[0][2] + sred2[0][3]);
+        y0 = (sred2[1][0] + sred2[1][1]) + (sred2[1][2] + sred2[1][3]);
+        s1 = (sred2[2][0] + sred2[2][1]) + (sred2[2][2] + sred2[2][3]);
+        y1 = (sred2[3][0] + sred2[3][1]) + (sred2[3][2] + sred2[3][3]);
+        __syncthreads();            // sred is free again for the caller's next group
+        const float inv0 = 1.0f / s0, inv1 = 1.0f / s1;
+        if (Ao) {
+            float* Ao1 = Ao + Nb;
+#pragma unroll
+            for (int k = 0; k < kSoftmaxRows; ++k) {
+                const int n = tid + 256 * k;
+                if (n < Nl) {
+                    Ao[n] = e0[k] * inv0;
+                    Ao1[n] = e1[k] * inv1;
+                }
+            }
+        }
+        if (active && tid == 0) { Yo[0] = y0 * inv0; Yo[1] = y1 * inv1; }
+        return;
+    }
+    float (*sr)[4] = reinterpret_cast<float (*)[4]>(sred);
+    for (int c = 0; c < C; ++c) {
+        if (Nb <= 256 * kSoftmaxRows) {
+            // the bag's logits of class c stay in registers: one read of logits and z, one exp
+            // per row (same per-thread order and reduction tree as the streaming path below)
+            float e[kSoftmaxRows];
+            float m = -INFINITY;
+#pragma unroll
+            for (int k = 0; k < kSoftmaxRows; ++k) {
+                const int n = tid + 256 * k;
+                e[k] = n < Nl ? lg[(size_t)n * C + c] : -INFINITY;
+                m = fmaxf(m, e[k]);
+            }
+            m = wave_max(m);
+            if (lane == 0) sr[0][wave] = m;
+            __syncthreads();
+            m = fmaxf(fmaxf(sr[0][0], sr[0][1]), fmaxf(sr[0][2], sr[0][3]));
+            __syncthreads();
+            float s = 0.f, y = 0.f;
+#pragma unroll
+            for (int k = 0; k < kSoftmaxRows; ++k) {
+                const int n = tid + 256 * k;
+                if (n < Nl) {
+                    e[k] = expf(e[k] - m);
+                    s += e[k];
+                    y = fmaf(e[k], zz[(size_t)n * C + c], y);
+                }
+            }
+            s = wave_sum(s);
+            y = wave_sum(y);
+            if (lane == 0) { sr[0][wave] = s; sr[1][wave] = y; }
+            __syncthreads();
+            s = (sr[0][0] + sr[0][1]) + (sr[0][2] + sr[0][3]);
+            y = (sr[1][0] + sr[1][1]) + (sr[1][2] + sr[1][3]);
+            __syncthreads();
+            const float inv = 1.0f / s;
+            if (Ao) {
+                float* Aoc = Ao + (size_t)c * Nb;
+#pragma unroll
+                for (int k = 0; k < kSoftmaxRows; ++k) {
+                    const int n = tid + 256 * k;
+                    if (n < Nl) Aoc[n] = e[k] * inv;
+                }
+            }
+            if (active && tid == 0) Yo[c] = y * inv;
+            continue;
+        }
+        float m = -INFINITY;
+        for (int n = tid; n < Nl; n += 256) m = fmaxf(m, lg[(size_t)n * C + c]);
+        m = wave_max(m);
+        if (lane == 0) sr[0][wave] = m;
+        __syncthreads();
+        m = fmaxf(fmaxf(sr[0][0], sr[0][1]), fmaxf(sr[0][2], sr[0][3]));
+        __syncthreads();
+        float s = 0.f, y = 0.f;
+        for (int n = tid; n < Nl; n += 256) {
+            const size_t o = (size_t)n * C + c;
+            const float e = expf(lg[o] - m);
+            s += e;
+            y = fmaf(e, zz[o], y);
+        }
+        s = wave_sum(s);
+        y = wave_sum(y);
+        if (lane == 0) { sr[0][wave] = s; sr[1][wave] = y; }
+        __syncthreads();
+        s = (sr[0][0] + sr[0][1]) + (sr[0][2] + sr[0][3]);
+        y = (sr[1][0] + sr[1][1]) + (sr[1][2] + sr[1][3]);
+        __syncthreads();
+        const float inv = 1.0f / s;
+        if (Ao) {
+            float* Aoc = Ao + (size_t)c * Nb;
+            for (int n = tid; n < Nl; n += 256) Aoc[n] = expf(lg[(size_t)n * C + c] - m) * inv;
+        }
+        if (active && tid == 0) Yo[c] = y * inv;
+    }
+}
+
+// softmax_pool_kernel: one 256-thread block per (t, bag) over the gate kernel's workspace.
+#ifndef MCGMIL_KERNELS_TEMPLATES_ONLY
+__global__ __launch_bounds__(256) void softmax_pool_kernel(const int32_t* bag_off, int T, int C,
+                                                           const float* logits, const float* zz,
+                                                           float* Y, float* A) {
+    __shared__ float sred[16];
+    const int t = blockIdx.x, b = blockIdx.y;
+    const int ob = bag_off[b];
+    const int Nb = bag_off[b + 1] - ob;
+    const size_t R0 = (size_t)T * ob + (size_t)t * Nb;
+    softmax_group(threadIdx.x, true, Nb, C, logits + R0 * C, zz + R0 * C,
+                  A ? A + (size_t)T * C * ob + (size_t)t * C * Nb : nullptr,
+                  Y + ((size_t)b * T + t) * C, sred);
+}
+#endif
 
 // ---------------------------------------------------------------------------------------
 // gate_pipe_kernel -- the fast path (gate tile pairs P <= 16, i.e. one pass: the reference's
@@ -389,26 +619,19 @@ __host__ __device__ constexpr size_t pipe_lds_bytes() {
            (size_t)MAXC * kPipeBM * 4 + (size_t)kRowInfo * kPipeBM * 4;
 }
 
-template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS>
-__global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParams p) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// One 128-row tile of the flattened (bag, t, n) space, rows R0 .. R0+127, whose row table is
+// already in `rinfo` (and visible: the caller's barrier). Scores go to lg_out / z_out at row
+// R0 + r - obase. LDS: Xs [2][SLOT] staging slots, red / zred the cross-wave reductions.
+template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS, bool EARLY_HV = true>
+__device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* Xs, float* red,
+                                          float* zred, const int* rinfo, float* lg_out,
+                                          float* z_out, long long obase) {
     constexpr int BM = kPipeBM;
     constexpr int RT = BM / 16;                     // 8 row tiles = 8 waves
     constexpr int NJ = 2 * PPW;
     constexpr int SLOT = RT * 64 * 8;               // elements of one 32-deep K step
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int KS = p.L >> 5;
-
-    E* Xs = reinterpret_cast<E*>(smem);                                   // [2][SLOT]
-    float* red = reinterpret_cast<float*>(smem + (size_t)2 * SLOT * sizeof(E));
-    float* zred = red + red_floats<BM, MAXC>();
-    int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);
-    const long long R0 = (long long)blockIdx.x * BM;
-
-    MCGMIL_STAMP(p, 0);
-    fill_row_table<BM>(p, R0, rinfo);
-    __syncthreads();
-    MCGMIL_STAMP(p, 1);
 
     // staging item of this thread: row wave*16 + (lane & 15), 8-chunk kq = lane >> 4 of
     // every K step; it lands at lane slot `lane` of row tile `wave` (= element tid*8)
@@ -543,7 +766,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     // bf16 separate heads: the epilogue's head vectors load under the K loop instead of after it
     // (+0.3-1.4% in same-process A/B, bitwise equal; profiles/r02/gate_ab.log). The fp32 kernel
     // has no registers to spare for them.
-    constexpr bool kEarlyHV = ONE_CLASS && sizeof(E) == 2;
+    constexpr bool kEarlyHV = EARLY_HV && ONE_CLASS && sizeof(E) == 2;
     HeadVec hvec[PPW];
     if constexpr (kEarlyHV) load_head_vectors<PPW>(p, q0, lane, hvec);
     // KS is even and >= 2 (host guarantees L % 64 == 0). The first two steps are peeled: their
@@ -570,8 +793,414 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     // ONE_CLASS: the wave's pairs all belong to gate q0 / (D/16) (idle waves: class >= C)
     const int one_class = ONE_CLASS ? (q0 < p.P ? q0 / (p.D >> 4) : MAXC) : -1;
     finish_scores<BM, MAXC>(p, R0, part, zacc, true, red, zred, rinfo, one_class,
-                            ONE_CLASS ? (p.D >> 4) / PPW : 0, false, true);
+                            ONE_CLASS ? (p.D >> 4) / PPW : 0, false, true, lg_out, z_out, obase);
     MCGMIL_STAMP(p, 7);
+}
+
+template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS>
+__global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int BM = kPipeBM;
+    E* Xs = reinterpret_cast<E*>(smem);                                   // [2][SLOT]
+    float* red = reinterpret_cast<float*>(smem + (size_t)2 * BM * 32 * sizeof(E));
+    float* zred = red + red_floats<BM, MAXC>();
+    int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);
+    const long long R0 = (long long)blockIdx.x * BM;
+
+    MCGMIL_STAMP(p, 0);
+    fill_row_table<BM>(p, R0, rinfo);
+    __syncthreads();
+    MCGMIL_STAMP(p, 1);
+    pipe_tile<E, PPW, MAXC, REPLAY, ONE_CLASS>(p, R0, Xs, red, zred, rinfo, p.logits, p.zz, 0);
+}
+
+// ---------------------------------------------------------------------------------------
+// gate_fused_kernel -- the whole hot path in ONE launch (model.py:280-316): gate scores,
+// softmax over instances and attention pooling. A workgroup owns a REGION: the t-groups
+// [t0, t1) of one bag, i.e. the contiguous flattened rows [S, S + (t1-t0)*N_b). It runs the
+// region's 128-row tiles one after the other through pipe_tile (the code of gate_pipe_kernel,
+// so the logits are bitwise the same), keeping the logits and classifier projections in LDS,
+// then runs softmax_group on each t-group, two at a time (threads 0-255 and 256-511): A and
+// Y are written once and no logit leaves the CU. Bags of more than fused_cap instances keep
+// one t-group per region and go through the global workspace instead (the workgroup re-reads
+// its own writes).
+// ---------------------------------------------------------------------------------------
+#ifndef MCGMIL_FUSED_FLATROWS
+#define MCGMIL_FUSED_FLATROWS 0
+#endif
+#ifndef MCGMIL_FUSED_GLOBAL
+#define MCGMIL_FUSED_GLOBAL 0      // diagnostic: every region's scores through the global workspace
+#endif
+#ifndef MCGMIL_FUSED_XCD
+#define MCGMIL_FUSED_XCD 1         // 1: regions of bag b on XCD b % 8 (uniform bags, B % 8 == 0)
+#endif
+#ifndef MCGMIL_FUSED_ROT
+#define MCGMIL_FUSED_ROT 0         // 1: a region's tiles start at 5 j mod ntiles (region_tile)
+#endif
+#ifndef MCGMIL_FUSED_PIPE
+#define MCGMIL_FUSED_PIPE 0        // 1: fused_region_tiles (cross-tile pipeline), 0: pipe_tile per tile
+#endif
+#ifndef MCGMIL_FUSED_EARLY_HV
+#define MCGMIL_FUSED_EARLY_HV 1   // head vectors before the K loop (as gate_pipe_kernel)
+#endif
+#ifndef MCGMIL_FUSED_CAP
+#define MCGMIL_FUSED_CAP 4096      // rows of one region's logits in LDS (C <= 2)
+#endif
+template <int MAXC>
+__host__ __device__ constexpr int fused_cap() { return MAXC <= 2 ? MCGMIL_FUSED_CAP : MCGMIL_FUSED_CAP / 4; }
+
+template <typename E, int MAXC>
+__host__ __device__ constexpr size_t fused_lds_bytes() {
+    return pipe_lds_bytes<E, MAXC>() + (size_t)kRowInfo * kPipeBM * 4   // second row table
+           + (size_t)2 * fused_cap<MAXC>() * MAXC * 4                   // logits + z of a region
+           + (size_t)2 * 16 * 4 + 64;                                   // softmax partials, region
+}
+
+// t-groups per region for a bag of Nb instances (the host sizes the grid with the same rule)
+__host__ __device__ inline int region_t_groups(int Nb, int T, int cap) {
+    if (Nb <= 0) return T;
+    if (Nb > cap) return 1;
+    const int ts = cap / Nb;
+    return ts < T ? ts : T;
+}
+
+struct Region {
+    int bag, t0, t1, Nb, ob;
+    int ntiles, rot;               // 128-row tiles; the first one this workgroup runs
+    long long S, rows;
+};
+
+// Tile i of a region's run order. Workgroups of one bag start at different tiles (rot = 5 j mod
+// ntiles for the bag's j-th region), so the ~32 of them on an XCD read different H rows at a
+// time and each 128-row chunk comes into that XCD's L2 once, for all of them. Started together
+// (rot = 0) they moved through the bag's rows in lockstep and every H load missed L2: the K loop
+// ran 34.4k cycles per tile against 24.1k in gate_pipe_kernel (profiles/r03/stamps_fused.log).
+__device__ __forceinline__ int region_tile(const Region& rg, int i) {
+    const int k = i + rg.rot;
+    return k < rg.ntiles ? k : k - rg.ntiles;
+}
+
+// The kernel's parameters (its only argument, at offset 0 of the kernarg segment) read again
+// through a pointer the compiler cannot see through, so the loads stay where they are used.
+__device__ __forceinline__ GateParams reload_kernarg_params(const GateParams& p) {
+#if __HIP_DEVICE_COMPILE__
+    typedef __attribute__((address_space(4))) const GateParams* KernargParams;
+    KernargParams q = (KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(q));
+    return *q;
+#else
+    return p;
+#endif
+}
+
+__device__ __forceinline__ bool decode_region(const GateParams& p, int g, int cap, Region& rg) {
+    int b, j, ts;
+    if (p.uniform_rows > 0) {
+        ts = p.region_t;
+        const int rpb = (p.T + ts - 1) / ts;
+        if (MCGMIL_FUSED_XCD && (p.B & 7) == 0) {
+            // workgroups g and g + 8 share an XCD (round-robin dispatch): XCD x = g & 7 takes the
+            // bags b = x (mod 8), so the ~32 workgroups of an XCD work on one bag's rows at a
+            // time and share its H rows in that XCD's L2
+            const int k = g >> 3;
+            b = 8 * (k / rpb) + (g & 7);
+            j = k - (k / rpb) * rpb;
+        } else {
+            b = g / rpb;
+            j = g - b * rpb;
+        }
+        if (b >= p.B) return false;
+    } else {
+        if (g >= p.region_off[p.B]) return false;
+        b = find_bag(p.region_off, p.B, 1, g);   // region counts are >= 1: strictly increasing
+        j = g - p.region_off[b];
+        ts = region_t_groups(p.bag_off[b + 1] - p.bag_off[b], p.T, cap);
+    }
+    rg.bag = b;
+    rg.ob = p.bag_off[b];
+    rg.Nb = p.bag_off[b + 1] - rg.ob;
+    rg.t0 = j * ts;
+    rg.t1 = rg.t0 + ts < p.T ? rg.t0 + ts : p.T;
+    rg.S = (long long)p.T * rg.ob + (long long)rg.t0 * rg.Nb;
+    rg.rows = (long long)(rg.t1 - rg.t0) * rg.Nb;
+    rg.ntiles = (int)((rg.rows + kPipeBM - 1) / kPipeBM);
+    rg.rot = MCGMIL_FUSED_ROT && rg.ntiles > 0 ? (int)(((long long)j * 5) % rg.ntiles) : 0;
+    return true;
+}
+
+// Row table of one tile of a region (rows past the region's end are padding).
+template <int BM>
+__device__ __forceinline__ void fill_row_table_region(const GateParams& p, const Region& rg,
+                                                      long long R0, int* rinfo) {
+    const int tid = threadIdx.x;
+    if (tid >= BM) return;
+    const long long rho = R0 + tid - rg.S;
+    int hrow = -1, t = 0, n = 0;
+    if (rho < rg.rows) {
+        const uint32_t r = (uint32_t)rho;          // a region is one t-group or <= fused_cap rows
+        const uint32_t tt = r / (uint32_t)rg.Nb;
+        n = (int)(r - tt * (uint32_t)rg.Nb);
+        t = rg.t0 + (int)tt;
+        hrow = rg.ob + n;
+    }
+    int* ri = rinfo + kRowInfo * tid;
+    ri[0] = hrow; ri[1] = t; ri[2] = n; ri[3] = rg.bag; ri[4] = rg.Nb;
+    ri[5] = (int)(p.bag_ids ? p.bag_ids[rg.bag] : p.bag_base + (uint32_t)rg.bag);
+}
+
+
+// ---------------------------------------------------------------------------------------
+// fused_region_tiles -- the region's tiles as ONE software pipeline (MCGMIL_FUSED_PIPE=1).
+// The K loop of pipe_tile prefetches H two steps and the weights one step ahead; in a region the
+// next tile's rows are known, so the prefetches of the last K steps fetch the NEXT tile's first H
+// chunks and step-0 weights, and the last step stages the next tile's step 0 (Philox included)
+// into the idle slot. The next tile's K loop then starts right after this tile's epilogue: no row
+// table, no prologue loads, no prologue barrier per tile. Row info is arithmetic (a region is
+// t-groups of one bag). The MFMA sequence, the masks and the epilogue are pipe_tile's, so the
+// logits are bitwise the same.
+// ---------------------------------------------------------------------------------------
+template <typename E>
+struct RowState {          // a thread's staging row (= its scoring row) in one tile
+    const E* hsrc;         // H row + its 8-element chunk kq (row 0 for padding rows)
+    uint32_t n, t;         // instance, sample (t_base included)
+    uint32_t inval;        // 0, or ~0 for a padding row (stages zeros, no score)
+};
+
+template <typename E>
+__device__ __forceinline__ RowState<E> region_row(const GateParams& p, const Region& rg, int tile,
+                                                 int srow, int kq) {
+    RowState<E> s;
+    const long long rho = (long long)tile * kPipeBM + srow;
+    const E* H = reinterpret_cast<const E*>(p.H);
+    if (rho < rg.rows) {
+        const uint32_t r = (uint32_t)rho;
+        const uint32_t tt = r / (uint32_t)rg.Nb;
+        s.n = r - tt * (uint32_t)rg.Nb;
+        s.t = (uint32_t)(p.t_base + rg.t0) + tt;
+        s.hsrc = H + (size_t)(rg.ob + (int)s.n) * p.ldh + kq * 8;
+        s.inval = 0u;
+    } else {
+        s.n = 0u;
+        s.t = 0u;
+        s.hsrc = H + kq * 8;
+        s.inval = 0xFFFFFFFFu;
+    }
+    return s;
+}
+
+template <typename E, int PPW, int MAXC, bool ONE_CLASS>
+__device__ __forceinline__ void fused_region_tiles(const GateParams& p0, Region* srg, int ntiles,
+                                                   E* Xs, float* red, float* zred, float* slg,
+                                                   float* szz) {
+    constexpr int BM = kPipeBM;
+    constexpr int RT = BM / 16;
+    constexpr int NJ = 2 * PPW;
+    constexpr int SLOT = RT * 64 * 8;
+    constexpr int CAP = fused_cap<MAXC>();
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kq = lane >> 4;
+    const int srow = wave * 16 + (lane & 15);
+
+    // the region's first tile: prologue loads and the staging of its step 0
+    Region rg0 = *srg;
+    const uint32_t cb = p0.bag_ids ? (uint32_t)p0.bag_ids[rg0.bag] : p0.bag_base + (uint32_t)rg0.bag;
+    RowState<E> cur = region_row<E>(p0, rg0, region_tile(rg0, 0), srow, kq);
+    const __amdgpu_buffer_rsrc_t wrs0 = make_rsrc(p0.Wp, p0.wp_bytes);
+    const int KS0 = p0.L >> 5;
+    const uint32_t tile_bytes0 = (uint32_t)KS0 * 512u * (uint32_t)sizeof(E);
+    const uint32_t lane_b = (uint32_t)lane * 8u * (uint32_t)sizeof(E);
+    const int q00 = __builtin_amdgcn_readfirstlane(wave) * PPW;
+    Frag<E> wA[NJ], wB[NJ], zA, zB;
+    Raw<E> hA, hB;
+    hA = load_raw(cur.hsrc);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        int q = q00 + (j >> 1);
+        q = q < p0.P ? q : p0.P - 1;
+        wA[j] = load_frag_buf<E>(wrs0, lane_b, (uint32_t)(2 * q + (j & 1)) * tile_bytes0);
+    }
+    zA = load_frag_buf<E>(wrs0, lane_b, (uint32_t)(2 * p0.P) * tile_bytes0);
+    hB = load_raw(cur.hsrc + 32);
+    {
+        const uint4 o = philox4x32_10<true>((uint32_t)kq, cur.n, cur.t, cb, p0.k0, p0.k1);
+        store_dropped(hA, o, p0.thrx_f, cur.inval, Xs + tid * 8);
+    }
+    __syncthreads();
+
+    for (int i = 0; i < ntiles; ++i) {
+        const GateParams p = reload_kernarg_params(p0);
+        Region* qr = srg;
+        asm volatile("" : "+v"(qr));
+        const Region rg = *qr;
+        const int KS = p.L >> 5;
+        const long long R0 = rg.S + (long long)region_tile(rg, i) * BM;
+
+        const __amdgpu_buffer_rsrc_t wrs = make_rsrc(p.Wp, p.wp_bytes);
+        const uint32_t tile_bytes = (uint32_t)KS * 512u * (uint32_t)sizeof(E);
+        constexpr uint32_t kStepBytes = 512u * (uint32_t)sizeof(E);
+        const int q0 = __builtin_amdgcn_readfirstlane(wave) * PPW;
+        uint32_t wsoff[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            int q = q0 + (j >> 1);
+            q = q < p.P ? q : p.P - 1;
+            wsoff[j] = (uint32_t)(2 * q + (j & 1)) * tile_bytes;
+        }
+        const uint32_t zsoff = (uint32_t)(2 * p.P) * tile_bytes;
+        auto wfrag = [&](uint32_t soff) { return load_frag_buf<E>(wrs, lane_b, soff); };
+
+        f32x4 acc[RT][NJ];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 zacc = {0.f, 0.f, 0.f, 0.f};
+
+        // K step s: MFMAs from slot `cur_slot`; weights of step s+1 (mod KS: the next tile's step 0
+        // at the last step), H of step s+2 and the staging of step s+1 from row state `hs` / `ss`
+        // (this tile's, or the next tile's once the step index wraps).
+        auto kstep = [&](int s, const E* cs, E* ns, const Frag<E> (&w)[NJ], const Frag<E>& z,
+                         Frag<E> (&wn)[NJ], Frag<E>& zn, const Raw<E>& h, Raw<E>& hn,
+                         const RowState<E>& hs, int hstep, const RowState<E>& ss, int sstep) {
+            const int s1 = s + 1 < KS ? s + 1 : 0;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) wn[j] = wfrag(wsoff[j] + (uint32_t)s1 * kStepBytes);
+            zn = wfrag(zsoff + (uint32_t)s1 * kStepBytes);
+            hn = load_raw(hs.hsrc + (size_t)hstep * 32);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                const Frag<E> x = load_frag(cs + (size_t)(rt * 64 + lane) * 8);
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[rt][j] = mma(w[j], x, acc[rt][j]);
+            }
+            const Frag<E> xz = load_frag(cs + (size_t)tid * 8);
+            zacc = mma(z, xz, zacc);
+            {
+                const uint4 o = philox4x32_10<true>((uint32_t)(sstep * 4 + kq), ss.n, ss.t, cb, p.k0, p.k1);
+                store_dropped(h, o, p.thrx_f, ss.inval, ns + tid * 8);
+            }
+            if constexpr (sizeof(E) == 2 && PPW == 2) {
+#pragma unroll
+                for (int k = 0; k < RT * NJ + 1; ++k) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0); // VALU
+                }
+            }
+            __syncthreads();
+        };
+
+        constexpr bool kEarlyHV = MCGMIL_FUSED_EARLY_HV && ONE_CLASS && sizeof(E) == 2;
+        HeadVec hvec[PPW];
+        if constexpr (kEarlyHV) load_head_vectors<PPW>(p, q0, lane, hvec);
+        // steps 0, 1 peeled (zero accumulators as inline constants), 2 .. KS-3 in pairs, and the
+        // last two peeled: their H prefetches and the last staging belong to the next tile
+        kstep(0, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA, cur, 2, cur, 1);
+        kstep(1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB, cur, 3, cur, 2);
+        for (int s = 2; s < KS - 2; s += 2) {
+            kstep(s, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA, cur, s + 2, cur, s + 1);
+            kstep(s + 1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB, cur, s + 3, cur, s + 2);
+        }
+        // the next tile's rows (this tile's again after the last one: loads in range, unused),
+        // computed here so that they are not live through the K loop
+        const RowState<E> nxt = region_row<E>(p, rg, region_tile(rg, i + 1 < ntiles ? i + 1 : i), srow, kq);
+        kstep(KS - 2, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA, nxt, 0, cur, KS - 1);
+        kstep(KS - 1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB, nxt, 1, nxt, 0);
+
+        float part[MAXC][RT];
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) part[c][rt] = 0.f;
+        fold_pairs<RT, PPW, MAXC, ONE_CLASS>(p, acc, q0, lane, part, kEarlyHV ? hvec : nullptr);
+        const int one_class = ONE_CLASS ? (q0 < p.P ? q0 / (p.D >> 4) : MAXC) : -1;
+        const bool lds = rg.Nb <= CAP && !MCGMIL_FUSED_GLOBAL;
+        score_rows<BM, MAXC>(p, R0, part, zacc, red, zred, one_class,
+                             ONE_CLASS ? (p.D >> 4) / PPW : 0, cur.inval == 0u, cur.t, cur.n, cb,
+                             lds ? slg : p.logits, lds ? szz : p.zz, lds ? rg.S : 0);
+        cur = nxt;
+    }
+}
+
+template <typename E, int PPW, int MAXC, bool ONE_CLASS>
+__global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GateParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int BM = kPipeBM;
+    constexpr int CAP = fused_cap<MAXC>();
+    E* Xs = reinterpret_cast<E*>(smem);                                   // [2][SLOT]
+    float* red = reinterpret_cast<float*>(smem + (size_t)2 * BM * 32 * sizeof(E));
+    float* zred = red + red_floats<BM, MAXC>();
+    int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);               // [2][kRowInfo * BM]
+    float* slg = reinterpret_cast<float*>(rinfo + 2 * kRowInfo * BM);    // [CAP][C]
+    float* szz = slg + CAP * MAXC;                                        // [CAP][C]
+    float* sred = szz + CAP * MAXC;                                       // [2][16]
+
+#if MCGMIL_DIAG & 64   // diagnostic (timing only): gate_pipe_kernel's work in this kernel's frame
+    {
+        const long long R0 = (long long)blockIdx.x * BM;
+        fill_row_table<BM>(p, R0, rinfo);
+        __syncthreads();
+        pipe_tile<E, PPW, MAXC, false, ONE_CLASS>(p, R0, Xs, red, zred, rinfo, p.logits, p.zz, 0);
+        return;
+    }
+#endif
+    Region rg;
+    if (!decode_region(p, (int)blockIdx.x, CAP, rg)) return;   // grid rounded up (ragged bags)
+    const int ntiles = (int)((rg.rows + BM - 1) / BM);
+    // The tile loop keeps almost nothing in registers across tiles: the region sits in LDS and
+    // the parameters are re-read from the kernarg segment in every tile, both through pointers
+    // the compiler cannot see through. Hoisted out of the loop, the ~40 scalar parameters and
+    // the region stay live across it, and the SGPR spills (into VGPR lanes) push the tile over
+    // 256 VGPRs.
+    Region* srg = reinterpret_cast<Region*>(sred + 32);
+    if (threadIdx.x == 0) *srg = rg;                 // read after the first tile's barrier
+#if MCGMIL_FUSED_PIPE
+    __syncthreads();                                 // the region in LDS
+    if (ntiles > 0) fused_region_tiles<E, PPW, MAXC, ONE_CLASS>(p, srg, ntiles, Xs, red, zred, slg, szz);
+#else
+    for (int i = 0; i < ntiles; ++i) {
+        Region* qr = srg;
+        asm volatile("" : "+v"(qr));
+        const GateParams pt = reload_kernarg_params(p);
+        // two row tables: tile i fills one while tile i-1's scoring may still read the other
+        int* ri = rinfo + (i & 1) * kRowInfo * BM;
+        MCGMIL_STAMP(pt, 0);
+        {
+            const Region r = *qr;
+#if MCGMIL_FUSED_FLATROWS   // diagnostic: the flat kernel's row table (uniform bags, whole tiles)
+            fill_row_table<BM>(pt, r.S + (long long)region_tile(r, i) * BM, ri);
+#else
+            fill_row_table_region<BM>(pt, r, r.S + (long long)region_tile(r, i) * BM, ri);
+#endif
+        }
+        __syncthreads();
+        MCGMIL_STAMP(pt, 1);
+        const Region r = *qr;
+        const bool lds = r.Nb <= CAP && !MCGMIL_FUSED_GLOBAL;
+        pipe_tile<E, PPW, MAXC, false, ONE_CLASS, MCGMIL_FUSED_EARLY_HV>(pt, r.S + (long long)region_tile(r, i) * BM, Xs, red, zred, ri,
+                                                  lds ? slg : pt.logits, lds ? szz : pt.zz,
+                                                  lds ? r.S : 0);
+    }
+#endif
+    __syncthreads();
+#if MCGMIL_DIAG & 32   // ablation (timing only, no A/Y): no softmax phase
+    if (ntiles >= 0) return;
+#endif
+    rg = *srg;
+    const bool in_lds = rg.Nb <= CAP && !MCGMIL_FUSED_GLOBAL;
+
+    // softmax + pooling per t-group (model.py:305-316), two groups at a time
+    const int G = rg.t1 - rg.t0;
+    const int half = threadIdx.x >> 8, ltid = threadIdx.x & 255;
+    for (int j0 = 0; j0 < G; j0 += 2) {
+        const bool act = j0 + half < G;
+        const int j = act ? j0 + half : j0;
+        const long long row0 = (long long)j * rg.Nb;                    // first row in the region
+        const float* lgj = in_lds ? slg + row0 * p.C : p.logits + (rg.S + row0) * p.C;
+        const float* zzj = in_lds ? szz + row0 * p.C : p.zz + (rg.S + row0) * p.C;
+        float* Ao = p.A ? p.A + (size_t)p.T * p.C * rg.ob + (size_t)(rg.t0 + j) * p.C * rg.Nb : nullptr;
+        float* Yo = p.Y + ((size_t)rg.bag * p.T + rg.t0 + j) * p.C;
+        softmax_group(ltid, act, rg.Nb, p.C, lgj, zzj, Ao, Yo, sred + half * 16);
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -703,170 +1332,8 @@ __global__ __launch_bounds__(kGateThreads) void gate_scores_kernel(const GatePar
         fold_pairs<RT, PPW, MAXC, false>(p, acc, q0, lane, part);
     }
     __syncthreads();   // every wave is done reading Xs: `red` may overwrite it
-    finish_scores<BM, MAXC>(p, R0, part, zacc, zwave, red, zred, rinfo, -1, 0, false, true);
-}
-
-// ---------------------------------------------------------------------------------------
-// softmax_pool_kernel: one 256-thread block per (t, bag). A = softmax over the bag's
-// instances (model.py:305), Y_c = sum_n A z_c (model.py:308-316).
-// ---------------------------------------------------------------------------------------
-constexpr int kSoftmaxRows = 16;    // register path for bags of up to 4096 instances
-
-__global__ __launch_bounds__(256) void softmax_pool_kernel(const int32_t* bag_off, int T, int C,
-                                                           const float* logits, const float* zz,
-                                                           float* Y, float* A) {
-    __shared__ float sred[2][4];
-    const int t = blockIdx.x, b = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int ob = bag_off[b];
-    const int Nb = bag_off[b + 1] - ob;
-    float* Yo = Y + ((size_t)b * T + t) * C;
-    if (Nb == 0) {
-        if (tid < C) Yo[tid] = 0.f;
-        return;
-    }
-    const size_t R0 = (size_t)T * ob + (size_t)t * Nb;
-    const size_t abase = (size_t)T * C * ob + (size_t)t * C * Nb;
-    if (C == 2 && Nb <= 256 * kSoftmaxRows) {
-        // The reference's two classes together: one 8-byte load per row of logits and of z, and
-        // the two classes' reductions share their barriers. Per class the arithmetic and its
-        // order are the register path's below, so A and Y are bitwise the same.
-        __shared__ float sred2[4][4];
-        float e0[kSoftmaxRows], e1[kSoftmaxRows];
-        float m0 = -INFINITY, m1 = -INFINITY;
-#pragma unroll
-        for (int k = 0; k < kSoftmaxRows; ++k) {
-            const int n = tid + 256 * k;
-            float2 l = make_float2(-INFINITY, -INFINITY);
-            if (n < Nb) l = *reinterpret_cast<const float2*>(logits + (R0 + n) * 2);
-            e0[k] = l.x;
-            e1[k] = l.y;
-            m0 = fmaxf(m0, e0[k]);
-            m1 = fmaxf(m1, e1[k]);
-        }
-        m0 = wave_max(m0);
-        m1 = wave_max(m1);
-        if (lane == 0) { sred2[0][wave] = m0; sred2[1][wave] = m1; }
-        __syncthreads();
-        m0 = fmaxf(fmaxf(sred2[0][0], sred2[0][1]), fmaxf(sred2[0][2], sred2[0][3]));
-        m1 = fmaxf(fmaxf(sred2[1][0], sred2[1][1]), fmaxf(sred2[1][2], sred2[1][3]));
-        __syncthreads();
-        float s0 = 0.f, y0 = 0.f, s1 = 0.f, y1 = 0.f;
-#pragma unroll
-        for (int k = 0; k < kSoftmaxRows; ++k) {
-            const int n = tid + 256 * k;
-            if (n < Nb) {
-                const float2 z = *reinterpret_cast<const float2*>(zz + (R0 + n) * 2);
-                e0[k] = expf(e0[k] - m0);
-                e1[k] = expf(e1[k] - m1);
-                s0 += e0[k];
-                s1 += e1[k];
-                y0 = fmaf(e0[k], z.x, y0);
-                y1 = fmaf(e1[k], z.y, y1);
-            }
-        }
-        s0 = wave_sum(s0);
-        y0 = wave_sum(y0);
-        s1 = wave_sum(s1);
-        y1 = wave_sum(y1);
-        if (lane == 0) {
-            sred2[0][wave] = s0; sred2[1][wave] = y0; sred2[2][wave] = s1; sred2[3][wave] = y1;
-        }
-        __syncthreads();
-        s0 = (sred2[0][0] + sred2[0][1]) + (sred2[0][2] + sred2[0][3]);
-        y0 = (sred2[1][0] + sred2[1][1]) + (sred2[1][2] + sred2[1][3]);
-        s1 = (sred2[2][0] + sred2[2][1]) + (sred2[2][2] + sred2[2][3]);
-        y1 = (sred2[3][0] + sred2[3][1]) + (sred2[3][2] + sred2[3][3]);
-        const float inv0 = 1.0f / s0, inv1 = 1.0f / s1;
-        if (A) {
-            float* Ao0 = A + abase;
-            float* Ao1 = Ao0 + Nb;
-#pragma unroll
-            for (int k = 0; k < kSoftmaxRows; ++k) {
-                const int n = tid + 256 * k;
-                if (n < Nb) {
-                    Ao0[n] = e0[k] * inv0;
-                    Ao1[n] = e1[k] * inv1;
-                }
-            }
-        }
-        if (tid == 0) { Yo[0] = y0 * inv0; Yo[1] = y1 * inv1; }
-        return;
-    }
-    for (int c = 0; c < C; ++c) {
-        if (Nb <= 256 * kSoftmaxRows) {
-            // the bag's logits of class c stay in registers: one read of logits and z, one exp
-            // per row (same per-thread order and reduction tree as the streaming path below)
-            float e[kSoftmaxRows];
-            float m = -INFINITY;
-#pragma unroll
-            for (int k = 0; k < kSoftmaxRows; ++k) {
-                const int n = tid + 256 * k;
-                e[k] = n < Nb ? logits[(R0 + n) * C + c] : -INFINITY;
-                m = fmaxf(m, e[k]);
-            }
-            m = wave_max(m);
-            if (lane == 0) sred[0][wave] = m;
-            __syncthreads();
-            m = fmaxf(fmaxf(sred[0][0], sred[0][1]), fmaxf(sred[0][2], sred[0][3]));
-            __syncthreads();
-            float s = 0.f, y = 0.f;
-#pragma unroll
-            for (int k = 0; k < kSoftmaxRows; ++k) {
-                const int n = tid + 256 * k;
-                if (n < Nb) {
-                    e[k] = expf(e[k] - m);
-                    s += e[k];
-                    y = fmaf(e[k], zz[(R0 + n) * C + c], y);
-                }
-            }
-            s = wave_sum(s);
-            y = wave_sum(y);
-            if (lane == 0) { sred[0][wave] = s; sred[1][wave] = y; }
-            __syncthreads();
-            s = (sred[0][0] + sred[0][1]) + (sred[0][2] + sred[0][3]);
-            y = (sred[1][0] + sred[1][1]) + (sred[1][2] + sred[1][3]);
-            __syncthreads();
-            const float inv = 1.0f / s;
-            if (A) {
-                float* Ao = A + abase + (size_t)c * Nb;
-#pragma unroll
-                for (int k = 0; k < kSoftmaxRows; ++k) {
-                    const int n = tid + 256 * k;
-                    if (n < Nb) Ao[n] = e[k] * inv;
-                }
-            }
-            if (tid == 0) Yo[c] = y * inv;
-            continue;
-        }
-        float m = -INFINITY;
-        for (int n = tid; n < Nb; n += 256) m = fmaxf(m, logits[(R0 + n) * C + c]);
-        m = wave_max(m);
-        if (lane == 0) sred[0][wave] = m;
-        __syncthreads();
-        m = fmaxf(fmaxf(sred[0][0], sred[0][1]), fmaxf(sred[0][2], sred[0][3]));
-        __syncthreads();
-        float s = 0.f, y = 0.f;
-        for (int n = tid; n < Nb; n += 256) {
-            const size_t o = (R0 + n) * C + c;
-            const float e = expf(logits[o] - m);
-            s += e;
-            y = fmaf(e, zz[o], y);
-        }
-        s = wave_sum(s);
-        y = wave_sum(y);
-        if (lane == 0) { sred[0][wave] = s; sred[1][wave] = y; }
-        __syncthreads();
-        s = (sred[0][0] + sred[0][1]) + (sred[0][2] + sred[0][3]);
-        y = (sred[1][0] + sred[1][1]) + (sred[1][2] + sred[1][3]);
-        __syncthreads();
-        const float inv = 1.0f / s;
-        if (A) {
-            float* Ao = A + abase + (size_t)c * Nb;
-            for (int n = tid; n < Nb; n += 256) Ao[n] = expf(logits[(R0 + n) * C + c] - m) * inv;
-        }
-        if (tid == 0) Yo[c] = y * inv;
-    }
+    finish_scores<BM, MAXC>(p, R0, part, zacc, zwave, red, zred, rinfo, -1, 0, false, true,
+                            p.logits, p.zz, 0);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -875,6 +1342,7 @@ __global__ __launch_bounds__(256) void softmax_pool_kernel(const int32_t* bag_of
 // coalesced over n -- and, in the trailing blocks, the mean class probability per (bag, c)
 // (infer.py:195 softmax over classes; net_utils.py:207-208 mean over T). Sums in fp64.
 // ---------------------------------------------------------------------------------------
+#ifndef MCGMIL_KERNELS_TEMPLATES_ONLY
 __global__ __launch_bounds__(256) void bag_stats_kernel(const int32_t* bag_off, int B, int T, int C,
                                                         long long total_rows, int stat_blocks,
                                                         const float* A, const float* Y,
@@ -916,6 +1384,7 @@ __global__ __launch_bounds__(256) void bag_stats_kernel(const int32_t* bag_off, 
     }
     P_mean[j] = (float)(acc / T);
 }
+#endif
 
 // ---------------------------------------------------------------------------------------
 // pack_weights_kernel: fp32 nn.Linear weights -> MFMA A-operand tiles of dtype E.
@@ -954,6 +1423,7 @@ __global__ void pack_weights_kernel(const float* Wv, const float* Wu, const floa
 // ---------------------------------------------------------------------------------------
 // Mask materialisation (parity tests): the exact decisions gate_scores_kernel draws.
 // ---------------------------------------------------------------------------------------
+#ifndef MCGMIL_KERNELS_TEMPLATES_ONLY
 __global__ void feature_keep_kernel(const int32_t* bag_off, int B, int T, int LC,
                                     long long total_samples, uint32_t k0, uint32_t k1,
                                     uint32_t bag_base, const uint32_t* bag_ids, int t_base,
@@ -975,7 +1445,9 @@ __global__ void feature_keep_kernel(const int32_t* bag_off, int B, int T, int LC
         out[i] = (uint8_t)keep_byte(o, thr);
     }
 }
+#endif
 
+#ifndef MCGMIL_KERNELS_TEMPLATES_ONLY
 __global__ void attention_keep_kernel(const int32_t* bag_off, int B, int T, int C,
                                       long long total, uint32_t k0, uint32_t k1,
                                       uint32_t bag_base, const uint32_t* bag_ids, int t_base,
@@ -995,5 +1467,6 @@ __global__ void attention_keep_kernel(const int32_t* bag_off, int B, int T, int 
                                 thr) ? 1 : 0;
     }
 }
+#endif
 
 }  // namespace mcgmil

@@ -11,8 +11,8 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(os.path.dirname(ROOT), "include")
 LIB = os.path.join(PKG, "libmcgmil.so")
-SOURCES = ["mcgmil.hip", "mcgmil_image.hip", "mcgmil_bn.hip", "mcgmil_conv.hip", "mcgmil_stem.hip"]
-DEPS = ["mcgmil.hip", "mcgmil_image.hip", "mcgmil_bn.hip", "mcgmil_conv.hip", "mcgmil_stem.hip", "mcgmil_kernels.h",
+SOURCES = ["mcgmil.hip", "mcgmil_fused.hip", "mcgmil_image.hip", "mcgmil_bn.hip", "mcgmil_conv.hip", "mcgmil_stem.hip"]
+DEPS = ["mcgmil.hip", "mcgmil_fused.hip", "mcgmil_fused.h", "mcgmil_image.hip", "mcgmil_bn.hip", "mcgmil_conv.hip", "mcgmil_stem.hip", "mcgmil_kernels.h",
         "mcgmil_device.h", "mcgmil_error.h", "mcgmil_gate_pp.h"]
 ARCH = os.environ.get("MCGMIL_OFFLOAD_ARCH", "gfx950")
 # No packed-fp32 VALU (v_pk_fma/mul/add_f32): with ROCm 7.2's compiler a packed write into the
@@ -23,7 +23,8 @@ DEVICE_FLAGS = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 # Per-source flags. The MCDO gate kernels are scheduled with LLVM's max-ILP strategy: +3.0% on the
 # bf16 separate-heads kernel and +1.1% shared, -1.8% on fp32 separate heads, measured in one process
 # with scripts/probe_gate.py (MCGMIL_PROBE_LIBS; profiles/r01/probe_sched.log). The convolution
-# and BatchNorm sources keep the default scheduler.
+# and BatchNorm sources keep the default scheduler, and so does mcgmil_fused.hip: under max-ILP its
+# tile loop spills (256 VGPRs + 64-220 B of scratch), with the default one it fits in 254.
 SOURCE_FLAGS = {"mcgmil.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
 
 

@@ -21,7 +21,7 @@ MCGMIL_U16 = 3
 EXPORTED = (
     "mcgmil_abi_version", "mcgmil_args_size", "mcgmil_last_error", "mcgmil_workspace_size",
     "mcgmil_packed_weights_size", "mcgmil_pack_weights", "mcgmil_mcdo_forward",
-    "mcgmil_gate_scores", "mcgmil_softmax_pool", "mcgmil_bag_stats", "mcgmil_feature_keep",
+    "mcgmil_gate_softmax_pool", "mcgmil_fused_regions", "mcgmil_gate_scores", "mcgmil_softmax_pool", "mcgmil_bag_stats", "mcgmil_feature_keep",
     "mcgmil_attention_keep",
     # include/mcgmil_image.h
     "mcgmil_image_args_size", "mcgmil_tile_grid", "mcgmil_image_workspace_size",
@@ -154,11 +154,13 @@ def bind(path: str, mcdo_only: bool = False):
         f.restype = ctypes.c_int
     L.mcgmil_pack_weights.argtypes = [pa, _vp, _vp]
     L.mcgmil_pack_weights.restype = ctypes.c_int
-    for name in ("mcgmil_mcdo_forward", "mcgmil_gate_scores", "mcgmil_softmax_pool",
-                 "mcgmil_bag_stats"):
+    for name in ("mcgmil_mcdo_forward", "mcgmil_gate_softmax_pool", "mcgmil_gate_scores",
+                 "mcgmil_softmax_pool", "mcgmil_bag_stats"):
         f = getattr(L, name)
         f.argtypes = [pa, _vp]
         f.restype = ctypes.c_int
+    L.mcgmil_fused_regions.argtypes = [pa, ctypes.POINTER(ctypes.c_int64)]
+    L.mcgmil_fused_regions.restype = ctypes.c_int
     for name in ("mcgmil_feature_keep", "mcgmil_attention_keep"):
         f = getattr(L, name)
         f.argtypes = [pa, _vp, _vp]

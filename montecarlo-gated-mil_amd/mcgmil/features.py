@@ -175,11 +175,32 @@ def conv2d(conv: nn.Conv2d, x: torch.Tensor, stats: bool = False,
     return (y, part) if stats else y
 
 
+def torch_conv(layer: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """The torch layer, with fp32 convolutions on the GPU split along the batch so that no call's
+    input or output reaches 2^31 bytes (MCGMIL_FP32_CONV_CHUNK=0: unsplit). On some MI355X boxes
+    the unsplit fp32 stem convolution of a config-5 bag (1,507 instances: a 4.85 GB output) came
+    back wrong from MIOpen -- features nrel 1.68 against the CPU, with this build's kernels off --
+    while other boxes matched the CPU to 2e-6 (scripts/probe_cfg5_drift.py)."""
+    if not (isinstance(layer, nn.Conv2d) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and x.shape[0] > 1 and os.environ.get("MCGMIL_FP32_CONV_CHUNK", "1") != "0"):
+        return layer(x)
+    oh = (x.shape[2] + 2 * layer.padding[0] - layer.dilation[0] * (layer.kernel_size[0] - 1) - 1) \
+        // layer.stride[0] + 1
+    ow = (x.shape[3] + 2 * layer.padding[1] - layer.dilation[1] * (layer.kernel_size[1] - 1) - 1) \
+        // layer.stride[1] + 1
+    per = 4 * max(x[0].numel(), layer.out_channels * oh * ow)
+    n = max(1, ((1 << 31) - 1) // per)
+    if n >= x.shape[0]:
+        return layer(x)
+    mf = torch.channels_last if x.is_contiguous(memory_format=torch.channels_last) else torch.contiguous_format
+    return torch.cat([layer(x[i:i + n]) for i in range(0, x.shape[0], n)]).contiguous(memory_format=mf)
+
+
 def run_conv(layer: nn.Module, x: torch.Tensor) -> torch.Tensor:
     """The backbone's convolution: the MFMA kernel when `conv_fusable`, else the torch layer."""
     if isinstance(layer, nn.Conv2d) and conv_fusable(layer, x):
         return conv2d(layer, x)
-    return layer(x)
+    return torch_conv(layer, x)
 
 
 def _f32(t: Optional[torch.Tensor], dev) -> Optional[torch.Tensor]:
@@ -432,7 +453,7 @@ def run_stem(conv: nn.Module, bn: nn.Module, pool: Optional[nn.Module], x: torch
         return stem(conv, bn, True, pool, x)
     if x.is_cuda and x.dim() == 4:
         x = x.contiguous(memory_format=torch.channels_last)
-    return bn_act(bn, conv(x), True, pool=pool)
+    return bn_act(bn, torch_conv(conv, x), True, pool=pool)
 
 
 class DeferredBN(NamedTuple):

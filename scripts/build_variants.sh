@@ -19,12 +19,13 @@ for spec in "$@"; do
     # per source, as mcgmil/_build.py: the gate kernels (mcgmil.hip) with the max-ILP scheduler
     (
         objs=""
-        srcs="mcgmil.hip mcgmil_image.hip mcgmil_bn.hip mcgmil_conv.hip mcgmil_stem.hip"
-        [ -n "${GATE_ONLY:-}" ] && srcs="mcgmil.hip"   # gate-kernel A/B: the MCDO entry points only
+        srcs="mcgmil.hip mcgmil_fused.hip mcgmil_image.hip mcgmil_bn.hip mcgmil_conv.hip mcgmil_stem.hip"
+        [ -n "${GATE_ONLY:-}" ] && srcs="mcgmil.hip mcgmil_fused.hip"   # gate-kernel A/B: the MCDO entry points only
         for f in $srcs; do
             [ -f "$src/$f" ] || continue
             extra=""
             [ "$f" = mcgmil.hip ] && extra="${GATE_SCHED--mllvm -amdgpu-sched-strategy=max-ilp}"
+            [ "$f" = mcgmil_fused.hip ] && extra="${FUSED_SCHED-}"
             nopk="-Xclang -target-feature -Xclang -packed-fp32-ops"
             [[ " $defs " == *" -DMCGMIL_PACKED=1 "* ]] && nopk=""   # packed-fp32 codegen on
             /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -c -fPIC -I"$inc" \

@@ -31,9 +31,14 @@ def main():
     img = C5.synthetic_mammogram(dev, seed=5)
     runs = []
     for mode in order:
+        # fp32torch: the fp32 pipeline with this build's BatchNorm kernels off (torch/MIOpen only)
+        os.environ["MCGMIL_FUSED_BN"] = "0" if mode == "fp32torch" else "1"
+        # fp32nochunk: the fp32 convolutions unsplit (features.torch_conv)
+        os.environ["MCGMIL_FP32_CONV_CHUNK"] = "0" if mode == "fp32nochunk" else "1"
         model.compute_dtype = torch.bfloat16 if mode == "bf16" else torch.float32
         o = mc_predict_image(model, patcher, img, T=100, seed=6,
                              features_dtype=torch.bfloat16 if mode == "bf16" else None)
+        os.environ["MCGMIL_FUSED_BN"] = "1"
         torch.cuda.synchronize()
         f = o["features"].double()
         print(f"{mode}: k={len(o['tiles_indices'])} features |max| {f.abs().max():.4g} "
@@ -43,6 +48,21 @@ def main():
     def nr(x, y):
         x, y = x.double(), y.double()
         return float((x - y).abs().max() / y.abs().max())
+
+    if os.environ.get("PROBE_CPU") == "1":   # the same instances through the ResNet on the host
+        from mcgmil.infer import IMAGENET_MEAN, IMAGENET_STD
+        inst, ids, _ = patcher.convert_img_to_bag(img, seed=6, out_dtype=torch.float32,
+                                                  normalize=(IMAGENET_MEAN, IMAGENET_STD))
+        torch.manual_seed(0)
+        cpu_model = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=False)
+        cpu_model.apply(deactivate_batchnorm)
+        cpu_model.load_state_dict({k: v.cpu() for k, v in model.state_dict().items()})
+        cpu_model.eval()
+        with torch.no_grad():
+            f_cpu = cpu_model.extract_features(inst.cpu()[None])[0]
+        print(f"cpu fp32: features |max| {f_cpu.abs().max():.4g} mean {f_cpu.mean():.4g}", flush=True)
+        for i, (m, o) in enumerate(runs):
+            print(f"run {i} ({m}) vs CPU fp32 features: nrel {nr(o['features'].cpu(), f_cpu):.3g}", flush=True)
 
     for ref_mode in ("fp32", "bf16"):
         ref = next((o for m, o in runs if m == ref_mode), None)

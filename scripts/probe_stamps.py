@@ -34,7 +34,7 @@ def main():
     dev = torch.device("cuda", 0)
     N, T, L, D, C = 2048, 100, 512, 128, 2
     B = int(os.environ.get("PROBE_BAGS", "16"))
-    for shared in (False, True):
+    for shared in ((False,) if os.environ.get("PROBE_FUSED") == "1" else (False, True)):
         G = 1 if shared else C
         arrays = synthetic.head_arrays(synthetic.head_state_dict(0, C=C, shared=shared), C, shared)
         head = ops.HeadTensors(*[torch.from_numpy(arrays[k]).to(dev) for k in ops.HeadTensors._fields])
@@ -51,11 +51,19 @@ def main():
         st = torch.zeros(tiles * 8, dtype=torch.int64, device=dev)
         a.debug = ctypes.c_void_p(st.data_ptr())
         sh = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        # PROBE_FUSED=1: the fused single launch (MCGMIL_FUSED=1; a region's last tile's stamps)
+        fused = os.environ.get("PROBE_FUSED") == "1"
+        if fused:
+            os.environ["MCGMIL_FUSED"] = "1"
+            lib.mcgmil_gate_softmax_pool.restype = ctypes.c_int
+            Y = torch.empty(B, T, C, device=dev)
+            a.Y = ctypes.c_void_p(Y.data_ptr())
+        launch = lib.mcgmil_gate_softmax_pool if fused else lib.mcgmil_gate_scores
         for _ in range(3):
-            assert lib.mcgmil_gate_scores(ctypes.byref(a), sh) == 0
+            assert launch(ctypes.byref(a), sh) == 0
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        assert lib.mcgmil_gate_scores(ctypes.byref(a), sh) == 0
+        assert launch(ctypes.byref(a), sh) == 0
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1)

@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined"
 HIPCC=${ROCM_PATH:-/opt/rocm}/bin/hipcc
 objs=()
-for f in mcgmil mcgmil_image mcgmil_bn mcgmil_conv mcgmil_stem; do
+for f in mcgmil mcgmil_fused mcgmil_image mcgmil_bn mcgmil_conv mcgmil_stem; do
     "$HIPCC" --offload-arch=gfx950 -std=c++17 -O1 -I"$REPO/include" $SAN \
         -Xclang -target-feature -Xclang -packed-fp32-ops \
         -c "$REPO/montecarlo-gated-mil_amd/csrc/$f.hip" -o "$OUT/$f.o" 2>&1 | grep -v "packed-fp32-ops" || true

@@ -72,9 +72,10 @@ def test_workspace_size_formula(hip_lib):
     packed = (2 * 16 + 1) * 16 * 512 * 2                     # (2P+1) tiles x KS x 512 x bf16
     scores = 100 * 2048 * 2 * 4
     plan = ((100 * 2048 // 16 * 4 + 255) // 256) * 256      # tile plan (int32 per 16-row tile)
-    assert n == ((packed + 255) // 256) * 256 + 2 * scores + plan
+    regions = 256                                            # fused region plan: int32 [B+1]
+    assert n == ((packed + 255) // 256) * 256 + 2 * scores + plan + regions
     rc, n2 = _ws(hip_lib, _args(packed_w=ctypes.c_void_p(0x2000)))
-    assert rc == 0 and n2 == 2 * scores + plan
+    assert rc == 0 and n2 == 2 * scores + plan + regions
 
 
 @pytest.mark.parametrize("field,value,code", [

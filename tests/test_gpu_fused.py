@@ -1,0 +1,154 @@
+"""The single-launch hot path (gate_fused_kernel via mcgmil_gate_softmax_pool, reference
+model.py:280-316) against the two-kernel path (gate_pipe_kernel -> workspace ->
+softmax_pool_kernel) and against the reference's golden outputs.
+
+Both paths run the same tile code and the same softmax_group, so every output must be BITWISE
+equal. The cases cover the fused kernel's region shapes: several t-groups per region (small N),
+one t-group per region (N = 2048 at cap 4096), bags larger than the LDS cap (logits through the
+global workspace, incl. > 4,096 instances: the streaming softmax), empty bags (Y = 0), ragged
+batches (the device region plan) and uniform ones (arithmetic region map), C = 1, 2, 4."""
+import contextlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import Case
+from oracle import mcdo_ref
+from mcgmil import synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@contextlib.contextmanager
+def fused(mode):
+    old = os.environ.get("MCGMIL_FUSED")
+    os.environ["MCGMIL_FUSED"] = mode
+    try:
+        yield
+    finally:
+        if old is None:
+            del os.environ["MCGMIL_FUSED"]
+        else:
+            os.environ["MCGMIL_FUSED"] = old
+
+
+def head_on(arrays, dev):
+    from mcgmil.ops import HeadTensors
+    return HeadTensors(*[torch.from_numpy(np.ascontiguousarray(arrays[k])).to(dev)
+                         for k in HeadTensors._fields])
+
+
+def regions(H, offs, head, T):
+    import ctypes
+    from mcgmil import _lib, ops
+    a = ops.make_args(H, offs, head, T, head.C, head.G, head.D, 0.1, 0.1, seed=1)
+    n = ctypes.c_size_t()
+    _lib.check(_lib.load().mcgmil_workspace_size(ctypes.byref(a), ctypes.byref(n)), "ws")
+    ws = torch.empty(max(n.value, 1), dtype=torch.uint8, device=H.device)
+    a.workspace, a.workspace_bytes = ctypes.c_void_p(ws.data_ptr()), n.value
+    Y = torch.empty(offs.numel() - 1, T, head.C, device=H.device)
+    a.Y = ctypes.c_void_p(Y.data_ptr())
+    r = ctypes.c_int64()
+    _lib.check(_lib.load().mcgmil_fused_regions(ctypes.byref(a), ctypes.byref(r)), "fused_regions")
+    return r.value
+
+
+CASES = [
+    # name, dtype, sizes, T, C, shared, D
+    ("bf16_sep_uniform_N2048", torch.bfloat16, [2048] * 3, 7, 2, False, 128),
+    ("bf16_sep_uniform_N300", torch.bfloat16, [300] * 4, 30, 2, False, 128),
+    ("bf16_sep_ragged", torch.bfloat16, [300, 0, 5000, 1, 129, 4096, 4097, 777], 5, 2, False, 128),
+    ("f32_sep_ragged", torch.float32, [17, 2048, 0, 640, 4100], 6, 2, False, 128),
+    ("f32_shared_uniform_N96", torch.float32, [96] * 5, 40, 2, True, 128),
+    ("f32_c4_sep_ragged", torch.float32, [50, 1500, 1024, 1025, 3], 4, 4, False, 64),
+    ("bf16_c1_ragged", torch.bfloat16, [33, 4000, 5], 9, 1, False, 128),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_fused_equals_two_kernel_path(cuda, case):
+    from mcgmil import ops
+    name, dtype, sizes, T, C, shared, D = case
+    L = 512
+    sd = synthetic.head_state_dict(5, L=L, D=D, C=C, shared=shared)
+    head = head_on(synthetic.head_arrays(sd, C, shared), cuda)
+    H = torch.cat([torch.from_numpy(synthetic.bag_features(60 + b, n, L)) for b, n in enumerate(sizes)]) \
+        .to(cuda).to(dtype).contiguous()
+    offs = ops.bag_offsets_tensor(sizes, cuda)
+    ids = torch.tensor([7 * b + 3 for b in range(len(sizes))], dtype=torch.int32, device=cuda)
+    kw = dict(p_feat=0.1, p_att=0.1, seed=1234, bag_ids=ids, return_stats=True)
+    with fused("0"):
+        assert regions(H, offs, head, T) == 0
+        ref = ops.mcdo_forward(H, offs, head, T, **kw)
+    with fused("1"):
+        nreg = regions(H, offs, head, T)
+        out = ops.mcdo_forward(H, offs, head, T, **kw)
+    torch.cuda.synchronize()
+    if dtype == torch.bfloat16 and (shared or C == 1):
+        assert nreg == 0           # bf16 heads of <= 8 gate tile pairs run gate_pp_kernel: not fused
+    else:
+        assert nreg > 0
+    for k in ref:
+        assert torch.equal(out[k], ref[k]) or (k == "A_var" and T == 1), k
+    # empty bags: Y = 0 (the reference would not produce a bag of 0 instances; the kernel's rule)
+    for b, n in enumerate(sizes):
+        if n == 0:
+            assert torch.count_nonzero(out["Y"][b]) == 0
+
+
+def test_fused_auto_policy(cuda):
+    """MCGMIL_FUSED=auto takes the fused launch only for batches of >= 16,384 regions: 16 bags of
+    N=2048, T=100 (800 regions of two t-groups) do not, 512 bags (25,600) do. Unset: never."""
+    from mcgmil import ops
+    sd = synthetic.head_state_dict(0, C=2, shared=False)
+    head = head_on(synthetic.head_arrays(sd, 2, False), cuda)
+    with fused("auto"):
+        small = torch.zeros(16 * 2048, 512, device=cuda, dtype=torch.bfloat16)
+        assert regions(small, ops.bag_offsets_tensor([2048] * 16, cuda), head, 100) == 0
+        big = torch.zeros(512 * 2048, 512, device=cuda, dtype=torch.bfloat16)
+        big_offs = ops.bag_offsets_tensor([2048] * 512, cuda)
+        assert regions(big, big_offs, head, 100) == 512 * 50
+    old = os.environ.pop("MCGMIL_FUSED", None)
+    try:
+        assert regions(big, big_offs, head, 100) == 0
+    finally:
+        if old is not None:
+            os.environ["MCGMIL_FUSED"] = old
+
+
+from test_gpu_parity import BF16_CASES, FP32_CASES, TOL32, TOL_BF16_IN, compare, run  # noqa: E402
+
+
+@pytest.mark.parametrize("name", FP32_CASES + BF16_CASES)
+def test_fused_matches_reference_goldens(cuda, name):
+    """The fused launch (forced) on every reference-made golden MC case, with the kernel's own
+    Philox masks, at the bounds of tests/test_gpu_parity.py (bf16 shared heads are not fused and
+    run the two-kernel path here)."""
+    case = Case(name)
+    bf16 = name in BF16_CASES
+    with fused("1"):
+        out = run(case, cuda, torch.bfloat16 if bf16 else torch.float32)
+    compare(case, out, TOL_BF16_IN if bf16 else TOL32)
+
+
+def test_fused_config3_bag_vs_oracle(cuda):
+    """One config-3 bag (N=2048, T=100, bf16 operands) through the fused launch against the CPU
+    oracle on the bf16-rounded inputs (the fp32 bounds x 10)."""
+    from mcgmil import ops
+    N, T, seed = 2048, 100, 77
+    sd = synthetic.head_state_dict(seed, C=2, shared=False)
+    Hn = synthetic.bf16_round(synthetic.bag_features(seed + 1, N))
+    head = head_on(synthetic.head_arrays(sd, 2, False), cuda)
+    with fused("1"):
+        out = ops.mcdo_forward(torch.from_numpy(Hn).to(cuda).bfloat16(), ops.bag_offsets_tensor([N], cuda),
+                               head, T, p_feat=0.1, p_att=0.1, seed=seed, bag_id_base=9, return_stats=True)
+    torch.cuda.synchronize()
+    kF, kA = mcdo_ref.masks_for_bag(seed, 9, T, N, 512, 2, 0.1, 0.1)
+    Yr, Ar = mcdo_ref.mc_inference(Hn, mcdo_ref.HeadParams(synthetic.head_arrays(
+        synthetic.round_state_dict_bf16(sd), 2, False)), kF, kA, 0.1, 0.1)
+    Yr, Ar = Yr.numpy()[:, 0], Ar.numpy()[:, 0]
+    np.testing.assert_allclose(out["Y"][0].cpu().numpy(), Yr, rtol=0, atol=1e-4)
+    A = out["A"].cpu().numpy().reshape(T, 2, N)
+    assert np.abs(A - Ar).max() / np.abs(Ar).max() <= 1e-4

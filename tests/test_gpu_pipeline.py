@@ -118,11 +118,13 @@ def test_mc_predict_image_bf16_features(cuda):
 
 # BASELINE config 5 itself (bench.py --workload cfg5: the 7036 x 2800 synthetic mammogram, 224-px
 # tiles at overlap 0.75 / empty_thresh 0.75, k = 1,507 instances, T = 100, the bench's model and
-# seed): the bf16 pipeline's uncertainty outputs against the fp32 pipeline's. Measured in round 2
-# (profiles/r02/bench_cfg5_bf16.log): A_mean nrel 9.9e-3, A_var nrel 4.1e-2, prob_mean 3.2e-5,
-# Y 7.2e-4, features nrel 2.8e-2. The bounds are 1.5x those. The drift enters in the backbone
-# (the bf16 ResNet moves the features by ~3% before the head; the bf16 head alone adds ~5e-3 to
-# A_mean, tests/test_gpu_parity.py::test_bf16_drift_vs_fp32_reference).
+# seed): the bf16 pipeline's uncertainty outputs against the fp32 pipeline's, whose features are
+# first checked against the same ResNet on the CPU. Measured in round 2
+# (profiles/r02/bench_cfg5_bf16.log) and again in round 3 (profiles/r03/probe_cfg5_drift.log):
+# A_mean nrel 9.9e-3, A_var nrel 4.1e-2, prob_mean 3.2e-5, Y 7.2e-4, features nrel 2.8e-2. The
+# bounds are 1.5x those. The drift enters in the backbone (the bf16 ResNet moves the features by
+# ~3% before the head; the bf16 head alone adds ~5e-3 to A_mean,
+# tests/test_gpu_parity.py::test_bf16_drift_vs_fp32_reference).
 CFG5_DRIFT = dict(A_mean=1.5 * 9.9e-3, A_var=1.5 * 4.1e-2, prob_mean=1.5 * 3.2e-5, Y=1.5 * 7.2e-4)
 
 
@@ -146,6 +148,21 @@ def test_cfg5_bf16_uncertainty_drift(cuda):
     a = mc_predict_image(model, patcher, img, T=100, seed=seed, features_dtype=None)
     assert len(a["tiles_indices"]) == 1507
     assert np.array_equal(a["tiles_indices"], b["tiles_indices"])
+
+    # the fp32 pipeline is the reference precision: its features against the CPU ResNet on the
+    # same instances (MIOpen's unsplit fp32 stem convolution of this bag came back wrong on some
+    # boxes, features nrel 1.68; features.torch_conv splits it, measured 2.4e-6)
+    from mcgmil.infer import IMAGENET_MEAN, IMAGENET_STD
+    inst, _, _ = patcher.convert_img_to_bag(img, seed=seed, out_dtype=torch.float32,
+                                            normalize=(IMAGENET_MEAN, IMAGENET_STD))
+    torch.manual_seed(0)
+    cpu_model = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=False)
+    cpu_model.apply(deactivate_batchnorm)
+    cpu_model.load_state_dict({k: v.cpu() for k, v in model.state_dict().items()})
+    cpu_model.eval()
+    with torch.no_grad():
+        f_cpu = cpu_model.extract_features(inst.cpu()[None])[0]
+    assert nrel(a["features"].cpu().numpy(), f_cpu.numpy()) <= 1e-4
 
     def nr(k):
         x, y = b[k].double(), a[k].double()
