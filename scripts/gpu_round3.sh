@@ -20,7 +20,7 @@ for s in ${STEPS:-fused all cfg5 bench}; do
         fused) step pytest_fused 300 python -u -m pytest tests/test_gpu_fused.py -m gpu -x -q -rf --timeout 120 --timeout-method thread ;;
         all) step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
         cfg5) step bench_cfg5 600 python bench.py --workload cfg5 --steps 5 --warmup 2 --no-cpu-baseline ;;
-        bench) step bench 600 python bench.py ;;
+        bench) step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
         bench16) step bench16 600 python bench.py --bags 16 --no-cpu-baseline ;;
         abfused) step ab_fused 300 env MCGMIL_PROBE_LIBS="$(ls -1 abvar/*.so abvar2/*.so 2>/dev/null | paste -sd, -)" python -u scripts/probe_fused.py ;;
         abfused128) step ab_fused128 300 env PROBE_N=128 MCGMIL_PROBE_LIBS="$(ls -1 abvar/*.so abvar2/*.so 2>/dev/null | paste -sd, -)" python -u scripts/probe_fused.py ;;
@@ -29,10 +29,10 @@ for s in ${STEPS:-fused all cfg5 bench}; do
                 step stamps_fused_flatrows 300 env PROBE_BAGS=128 PROBE_FUSED=1 STAMP_DEFINES=MCGMIL_FUSED_PIPE=0,MCGMIL_FUSED_FLATROWS=1 python -u scripts/probe_stamps.py ;;
         listpmc) step list_pmc 120 rocprofv3 --list-avail ;;
         drift) step probe_drift 600 env PROBE_CPU=1 python -u scripts/probe_cfg5_drift.py bf16 fp32 fp32nochunk fp32torch ;;
-        pmc) step pmc 1200 bash scripts/pmc_passes.sh ;;
+        pmc) step pmc 1100 bash scripts/pmc_passes.sh ;;
         pmcab) step pmc_ab 1200 env PROBE_ROUNDS=1 PMC_CMD="python3 scripts/probe_fused.py" bash scripts/pmc_passes.sh ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-        prof) rm -rf "$OUT/prof"; step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py
+        prof) rm -rf "$OUT/prof"; step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5
               find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \; ;;
     esac
 done
