@@ -10,9 +10,12 @@ Reference lines restated (xkuubix/MonteCarlo-Gated-MIL):
   net_utils.py:207-210  mc_test: softmax -> mean over passes -> argmax
   infer.py:216-219    attention mean and torch's unbiased std over passes (var = std^2)
 
-Parity: these are single numpy/torch reductions with the reference's own argument choices;
-they are pinned by restatement (the reference scripts import neptune/matplotlib/torchvision,
-which this image lacks, so the functions cannot be run directly here).
+Parity: pinned. The reference's own plot_attention_and_density (infer.py:14-92) was run on the
+reference's MC logits (and seeded random ones) by tests/golden/make_golden_stats.py, which
+compiles only that function from /root/reference/infer.py (the module itself imports neptune,
+matplotlib and the DICOM dataset, absent here) and captures its mean/median/std/IQR/min/max and
+mean entropy from a recording matplotlib stand-in; tests/golden/caller_stats_ref.npz holds them
+and tests/test_caller_stats.py checks this restatement against them (|diff| <= 1e-6).
 """
 import numpy as np
 

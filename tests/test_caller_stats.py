@@ -49,3 +49,49 @@ def test_oracle_matches_numpy_definitions():
     assert abs(s["pos_std"] - np.sqrt(np.mean((pos - pos.mean()) ** 2))) < 1e-6
     assert abs(s["mean_entropy"] - np.mean(-np.sum(p * np.log(p + 1e-10), -1))) < 1e-6
     assert s["prediction"] == int(np.argmax(p.mean(0)))
+
+
+def _reference_stats():
+    """tests/golden/caller_stats_ref.npz: the scalars the reference's own plot_attention_and_density
+    computed (infer.py:47-57, captured by tests/golden/make_golden_stats.py) on the reference's
+    MC logits and on seeded random logits."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "caller_stats_ref.npz"))
+    keys = [str(k) for k in z["keys"]]
+    for i, name in enumerate(z["names"]):
+        T = int(z["T"][i])
+        yield str(name), z["Y"][i, :T], dict(zip(keys, z["stats"][i].tolist()))
+
+
+# reference local name (infer.py:49-57) -> caller_stats / uncertainty_summary key
+REF_KEYS = {"mean_pred": "pos_mean", "median_pred": "pos_median", "std_pred": "pos_std",
+            "iqr_pred": "pos_iqr", "min_pred": "pos_min", "max_pred": "pos_max",
+            "mean_entropy": "mean_entropy"}
+
+
+def test_oracle_matches_reference_scalars():
+    """The restatement against the reference's own numbers (pinned, not restated)."""
+    n = 0
+    for name, Y, ref in _reference_stats():
+        got = caller_stats.caller_stats(Y)
+        for rk, k in REF_KEYS.items():
+            assert abs(got[k] - ref[rk]) <= 1e-6, (name, k, got[k], ref[rk])
+        n += 1
+    assert n == 10
+
+
+def _summary_matches_reference(device):
+    from mcgmil.infer import uncertainty_summary
+    for name, Y, ref in _reference_stats():
+        got = uncertainty_summary(torch.from_numpy(Y).to(device))
+        for rk, k in REF_KEYS.items():
+            assert abs(got[k] - ref[rk]) <= 1e-6, (name, k, got[k], ref[rk])
+
+
+def test_summary_matches_reference_scalars_cpu():
+    _summary_matches_reference("cpu")
+
+
+@pytest.mark.gpu
+def test_summary_matches_reference_scalars_gpu():
+    _summary_matches_reference("cuda")
