@@ -14,9 +14,10 @@ META = ("N", "T", "C", "L", "D", "shared", "p_f", "p_a", "h_seed", "w_seed", "ma
 
 
 def names(prefix=""):
-    """MCDO head golden cases (the patcher_* fixtures belong to tests/test_patcher_oracle.py)."""
+    """MCDO head golden cases (the patcher_* fixtures belong to tests/test_patcher_oracle.py, the
+    caller_stats_* ones to tests/test_caller_stats.py)."""
     return sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, prefix + "*.npz"))
-                  if not os.path.basename(f).startswith("patcher_"))
+                  if not os.path.basename(f).startswith(("patcher_", "caller_stats_")))
 
 
 class Case:
