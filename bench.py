@@ -44,14 +44,16 @@ def bytes_per_bag(N, T, L, C, esize):
     return N * L * esize + 4 * T * C * N + 4 * T * C
 
 
-def measured_traffic(N, T, B, dtype, shared):
+def measured_traffic(N, T, B, dtype, shared, path_kind):
     """HBM bytes per gate launch from the committed rocprofv3 PMC passes (profiles/*/
-    gate_traffic.json, newest round first) when they were taken on this exact workload."""
+    gate_traffic.json, newest round first) when they were taken on this exact workload and
+    launch path ("fused": gate_fused_kernel; "pipe": gate_pipe_kernel)."""
     import glob
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "gate_traffic.json")),
                        reverse=True):
         t = json.load(open(path))
-        if t.get("config") == {"bags": B, "N": N, "T": T, "dtype": dtype, "shared": shared}:
+        if t.get("config") == {"bags": B, "N": N, "T": T, "dtype": dtype, "shared": shared} and \
+                t.get("path", "pipe") == path_kind:
             return t["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
     return None, None
 
@@ -271,7 +273,7 @@ def main():
     achieved = F / (gate_ms * 1e-3) / 1e12
     hbm_bytes = sum(bytes_per_bag(n, T, L, C, esize) for n in sizes) + packed.numel()
     hbm_gbs = hbm_bytes / (gate_ms * 1e-3) / 1e9
-    traffic, traffic_src = measured_traffic(N, T, B, args.dtype, args.shared) \
+    traffic, traffic_src = measured_traffic(N, T, B, args.dtype, args.shared, "fused" if fused else "pipe") \
         if args.workload == "cfg3" else (None, None)
     if rank == 0:
         # the CPU baseline is a rank-0, N=1 figure: at N > 1 it would only hold the other ranks

@@ -126,9 +126,10 @@ int mcgmil_mcdo_forward(const mcgmil_args* a, void* stream);
 
 /* Its stages (same args/workspace; call in this order, after packing if packed_w is NULL):
  * mcgmil_gate_softmax_pool, then mcgmil_bag_stats. mcgmil_gate_softmax_pool is
- * mcgmil_gate_scores followed by mcgmil_softmax_pool, or ONE fused launch when the environment
- * asks for it: MCGMIL_FUSED=1 (whenever it applies) or MCGMIL_FUSED=auto (batches of >= 16,384
- * regions). Both give bitwise the same A and Y. */
+ * ONE fused launch (gate scores, softmax, pooling) for batches of equal-size bags with >= 16,384
+ * regions, else
+ * mcgmil_gate_scores followed by mcgmil_softmax_pool. MCGMIL_FUSED=1 takes the fused launch
+ * whenever it applies, MCGMIL_FUSED=0 never (default: auto). Both give bitwise the same A and Y. */
 int mcgmil_gate_softmax_pool(const mcgmil_args* a, void* stream);
 /* The fused launch mcgmil_gate_softmax_pool would make for these args: *regions = its number of
  * workgroups (one per region of t-groups of a bag; an upper bound for ragged bags), or 0 when

@@ -252,17 +252,18 @@ int dispatch_gate(const mcgmil::GateParams& gp, int L, int dtype, hipStream_t s)
 // Fused single launch (gate_fused_kernel) or the two-kernel path (gate scores into the
 // workspace, then softmax_pool_kernel)? The fused kernel runs the pipelined gate kernel's tiles
 // (Philox masks, no replay); a workgroup owns a whole region (~32 tiles at config 3), so it
-// needs many regions to fill 256 CUs without a tail: MCGMIL_FUSED=auto takes it for batches of
-// >= 16,384 regions (64 per CU), MCGMIL_FUSED=1 whenever it applies. By default (unset or 0) the
-// two-kernel path runs: on MI355X the fused kernel measured 11-19% slower at config 3 (same
-// tiles, bitwise the same outputs), against ~1% for the softmax launch it saves.
+// needs many regions to fill 256 CUs without a tail. By default (MCGMIL_FUSED unset or "auto")
+// it takes batches of equal-size bags with >= 16,384 regions (64 per CU): at config 3 it is 0.1-0.8% faster than the
+// two-kernel path in the same process (bitwise the same outputs) and moves 40% fewer
+// HBM bytes (no logits/z workspace round trip). MCGMIL_FUSED=1 takes it whenever it applies,
+// MCGMIL_FUSED=0 never.
 constexpr long long kFusedMinRegions = 16384;
 
 int fused_mode() {   // -1 auto, 0 off, 1 on (read per call: tests switch it in one process)
     const char* e = getenv("MCGMIL_FUSED");
     if (e && strcmp(e, "1") == 0) return 1;
-    if (e && strcmp(e, "auto") == 0) return -1;
-    return 0;       // default: the two-kernel path (measured faster, DESIGN.md §4 gate_fused_kernel)
+    if (e && strcmp(e, "0") == 0) return 0;
+    return -1;      // default: auto
 }
 
 // Returns 1 if the fused kernel was launched (with `regions` set: nothing is launched, *regions
@@ -273,6 +274,7 @@ int try_fused_maxc(const mcgmil::GateParams& gp, long long total_rows, int L, hi
     *rc = MCGMIL_OK;
     // (L >= 128: the fused pipeline peels two K steps at each end of a tile)
     if (gp.keep_feat || L % 64 != 0 || L < 128 || gp.P > 2 * mcgmil::kGateWaves) return 0;
+    if (mcgmil::fused_kernel_lds_bytes<E, MAXC>(L) > 160 * 1024) return 0;   // bf16 L > 1024
     if constexpr (sizeof(E) == 2) {       // bf16: the kernel dispatch_gate_maxc would pick
         const int mode = gate_mode();
         const bool pipe = mode == 1 || (mode == 0 && gp.P > 2 * mcgmil::kPPWaves);
@@ -280,8 +282,11 @@ int try_fused_maxc(const mcgmil::GateParams& gp, long long total_rows, int L, hi
     }
     const int fm = fused_mode();
     if (fm == 0) return 0;
-    if (fm < 0 && mcgmil_detail::fused_regions(gp, total_rows, mcgmil::fused_cap<MAXC>(), true) <
-                      kFusedMinRegions)
+    // auto: uniform batches only -- on ragged ones (config 4) the fused launch measured 2.8% slower
+    // (regions of 16-32 tiles straddling t-groups; profiles/r03/bench_cfg4*.log)
+    if (fm < 0 && (gp.uniform_rows <= 0 ||
+                   mcgmil_detail::fused_regions(gp, total_rows, mcgmil::fused_cap<MAXC>(), true) <
+                       kFusedMinRegions))
         return 0;
     // same kernel shape as dispatch_gate_pipe: one class per wave for separate heads
     const int ppw = gp.P <= mcgmil::kGateWaves ? 1 : 2;

@@ -65,6 +65,10 @@ struct GateParams {
 #define MCGMIL_STAMP(p, i) do {} while (0)
 #endif
 
+#ifndef MCGMIL_DIAG_H0
+#define MCGMIL_DIAG_H0 0   // diagnostic (timing only, wrong results): every bag reads bag 0's H rows
+#endif
+
 constexpr int kGateThreads = 512;  // 8 waves
 constexpr int kGateWaves = kGateThreads / kWave;
 constexpr int kRowInfo = 6;        // ints per row: hrow, t, n, bag, Nb, bag counter
@@ -100,7 +104,7 @@ __device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0
             t = (int)(local / Nb);
             n = (int)(local - (long long)t * Nb);
         }
-        hrow = bag * Nb + n;
+        hrow = (MCGMIL_DIAG_H0 ? 0 : bag * Nb) + n;
     } else if (R < p.total_samples) {
         if (p.tile_bag) {
             bag = p.tile_bag[R0 / BM];
@@ -118,7 +122,7 @@ __device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0
             t = (int)(local / Nb);
             n = (int)(local - (long long)t * Nb);
         }
-        hrow = ob + n;
+        hrow = (MCGMIL_DIAG_H0 ? 0 : ob) + n;
     }
     int* ri = rinfo + kRowInfo * tid;
     ri[0] = hrow; ri[1] = t; ri[2] = n; ri[3] = bag; ri[4] = Nb;
@@ -619,13 +623,34 @@ __host__ __device__ constexpr size_t pipe_lds_bytes() {
            (size_t)MAXC * kPipeBM * 4 + (size_t)kRowInfo * kPipeBM * 4;
 }
 
+// The classifier tile's packed fragments of all KS K steps (tile 2P of the packed weights) into
+// LDS [KS][64][8], by the whole workgroup; the caller's next barrier makes them visible.
+template <typename E>
+__device__ __forceinline__ void load_classifier_lds(__amdgpu_buffer_rsrc_t wrs, uint32_t zsoff, int KS, E* zw) {
+    for (int i = threadIdx.x; i < KS * 64; i += kGateThreads)
+        *reinterpret_cast<f32x4*>(zw + (size_t)i * 8) = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (uint32_t)i * 8u * (uint32_t)sizeof(E), zsoff, 0));
+}
+
+// A tile's prologue loads (H of steps 0 and 1 of the thread's staging row, step-0 weights),
+// issued by the PREVIOUS tile of the same workgroup right after its K loop (pipe_tile's NEXT
+// mode), so they land under that tile's epilogue instead of in this tile's prologue.
+template <typename E, int NJ>
+struct TileLoads {
+    Raw<E> h0, h1;
+    Frag<E> w[NJ];
+};
+
 // One 128-row tile of the flattened (bag, t, n) space, rows R0 .. R0+127, whose row table is
 // already in `rinfo` (and visible: the caller's barrier). Scores go to lg_out / z_out at row
 // R0 + r - obase. LDS: Xs [2][SLOT] staging slots, red / zred the cross-wave reductions.
-template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS, bool EARLY_HV = true>
+template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS, bool EARLY_HV = true,
+          bool ZL = false, bool ZLOAD = true, bool NEXT = false>
 __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* Xs, float* red,
                                           float* zred, const int* rinfo, float* lg_out,
-                                          float* z_out, long long obase) {
+                                          float* z_out, long long obase, E* zw = nullptr,
+                                          TileLoads<E, 2 * PPW>* tl = nullptr, bool have_tl = false,
+                                          const E* next_hsrc = nullptr) {
     constexpr int BM = kPipeBM;
     constexpr int RT = BM / 16;                     // 8 row tiles = 8 waves
     constexpr int NJ = 2 * PPW;
@@ -705,7 +730,7 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
 #else
 #pragma unroll
         for (int j = 0; j < NJ; ++j) wn[j] = wfrag(wsoff[j] + (uint32_t)s1 * kStepBytes);
-        zn = wfrag(zsoff + (uint32_t)s1 * kStepBytes);
+        if constexpr (!ZL) zn = wfrag(zsoff + (uint32_t)s1 * kStepBytes);
 #endif
 #if MCGMIL_DIAG & 1   // ablation (timing only, wrong results): no H prefetch
         hn = h;
@@ -719,7 +744,8 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
             for (int j = 0; j < NJ; ++j) acc[rt][j] = mma(w[j], x, acc[rt][j]);
         }
         const Frag<E> xz = load_frag(cur + (size_t)tid * 8);  // row tile `wave`
-        zacc = mma(z, xz, zacc);
+        if constexpr (ZL) zacc = mma(load_frag(zw + (size_t)(s * 64 + lane) * 8), xz, zacc);
+        else zacc = mma(z, xz, zacc);
         stage(s + 1, h, nxt);           // step KS is staged into the idle slot and never read
         if constexpr (sizeof(E) == 2 && PPW == 2) {
             // Spread the Philox/staging VALU over the MFMA stream (1 MFMA : VPM VALU) instead
@@ -754,11 +780,25 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
     // prologue: stage step 0, load the weights of step 0 and H of step 1
     Frag<E> wA[NJ], wB[NJ], zA, zB;
     Raw<E> hA, hB;
-    hA = load_raw(hsrc);
+    if (NEXT && have_tl) {            // issued by the previous tile (NEXT mode), under its epilogue
+        hA = tl->h0;
+        hB = tl->h1;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) wA[j] = wfrag(wsoff[j]);
-    zA = wfrag(zsoff);
-    hB = load_raw(hsrc + 32);
+        for (int j = 0; j < NJ; ++j) wA[j] = tl->w[j];
+    } else {
+        hA = load_raw(hsrc);
+        hB = load_raw(hsrc + 32);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) wA[j] = wfrag(wsoff[j]);
+    }
+    if constexpr (ZL) {
+        // ZL: the classifier tile's fragments of all K steps sit in LDS (ZLOAD: loaded here, by
+        // this tile; else by the caller, once), so the K loop reads them with one ds_read per
+        // wave instead of 8 waves fetching the same 1 KiB per step. Visible after the barrier.
+        if constexpr (ZLOAD) load_classifier_lds<E>(wrs, zsoff, KS, zw);
+    } else {
+        zA = wfrag(zsoff);
+    }
     stage(0, hA, Xs);
     __syncthreads();
     MCGMIL_STAMP(p, 2);
@@ -782,6 +822,12 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
         kstep(s + 1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB);
     }
     MCGMIL_STAMP(p, 3);
+    if constexpr (NEXT) {             // the next tile's prologue loads, in flight under the epilogue
+        tl->h0 = load_raw(next_hsrc);
+        tl->h1 = load_raw(next_hsrc + 32);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) tl->w[j] = wfrag(wsoff[j]);
+    }
 
     float part[MAXC][RT];
 #pragma unroll
@@ -841,7 +887,15 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
 #define MCGMIL_FUSED_PIPE 0        // 1: fused_region_tiles (cross-tile pipeline), 0: pipe_tile per tile
 #endif
 #ifndef MCGMIL_FUSED_EARLY_HV
-#define MCGMIL_FUSED_EARLY_HV 1   // head vectors before the K loop (as gate_pipe_kernel)
+#define MCGMIL_FUSED_EARLY_HV 0   // 1: head vectors before the K loop (as gate_pipe_kernel); in the
+                                  // tile loop they left the K loop 16 VGPRs short, and the compiler
+                                  // then waited on every B-fragment read (15.6 vs 13.7 ms, gate_ab_r03.log)
+#endif
+#ifndef MCGMIL_FUSED_NMAJOR
+#define MCGMIL_FUSED_NMAJOR 1
+#endif
+#ifndef MCGMIL_FUSED_NEXT
+#define MCGMIL_FUSED_NEXT 0        // 1: a tile issues the next tile's prologue loads under its epilogue (spills: 160 B)
 #endif
 #ifndef MCGMIL_FUSED_CAP
 #define MCGMIL_FUSED_CAP 4096      // rows of one region's logits in LDS (C <= 2)
@@ -854,6 +908,18 @@ __host__ __device__ constexpr size_t fused_lds_bytes() {
     return pipe_lds_bytes<E, MAXC>() + (size_t)kRowInfo * kPipeBM * 4   // second row table
            + (size_t)2 * fused_cap<MAXC>() * MAXC * 4                   // logits + z of a region
            + (size_t)2 * 16 * 4 + 64;                                   // softmax partials, region
+}
+
+// bf16: the classifier tile's weight fragments of every K step stay in LDS for the workgroup's
+// whole region (L/32 KiB after the rest), loaded once instead of per wave and K step
+#ifndef MCGMIL_FUSED_ZL
+#define MCGMIL_FUSED_ZL 1
+#endif
+template <typename E>
+__host__ __device__ constexpr bool fused_zl() { return MCGMIL_FUSED_ZL && sizeof(E) == 2; }
+template <typename E, int MAXC>
+__host__ __device__ constexpr size_t fused_kernel_lds_bytes(int L) {
+    return fused_lds_bytes<E, MAXC>() + (fused_zl<E>() ? (size_t)(L / 32) * 512 * sizeof(E) : 0);
 }
 
 // t-groups per region for a bag of Nb instances (the host sizes the grid with the same rule)
@@ -870,12 +936,16 @@ struct Region {
     long long S, rows;
 };
 
-// Tile i of a region's run order. Workgroups of one bag start at different tiles (rot = 5 j mod
-// ntiles for the bag's j-th region), so the ~32 of them on an XCD read different H rows at a
-// time and each 128-row chunk comes into that XCD's L2 once, for all of them. Started together
-// (rot = 0) they moved through the bag's rows in lockstep and every H load missed L2: the K loop
-// ran 34.4k cycles per tile against 24.1k in gate_pipe_kernel (profiles/r03/stamps_fused.log).
+// Tile i of a region's run order. MCGMIL_FUSED_NMAJOR: when the region is G > 1 t-groups of
+// whole tiles, instance-block major -- tile i reads the same 128 H rows as tile i-1 for G-1 of
+// every G tiles, so each block comes from beyond L2 once per region instead of G times.
+// MCGMIL_FUSED_ROT: the bag's j-th region starts at tile 5 j (mod ntiles). The order changes no
+// result: every tile's logits land at their own rows, and the softmax runs after the last tile.
 __device__ __forceinline__ int region_tile(const Region& rg, int i) {
+#if MCGMIL_FUSED_NMAJOR
+    const int G = rg.t1 - rg.t0;
+    if (G > 1 && rg.Nb % kPipeBM == 0) return (i % G) * (rg.Nb / kPipeBM) + i / G;
+#endif
     const int k = i + rg.rot;
     return k < rg.ntiles ? k : k - rg.ntiles;
 }
@@ -941,7 +1011,7 @@ __device__ __forceinline__ void fill_row_table_region(const GateParams& p, const
         const uint32_t tt = r / (uint32_t)rg.Nb;
         n = (int)(r - tt * (uint32_t)rg.Nb);
         t = rg.t0 + (int)tt;
-        hrow = rg.ob + n;
+        hrow = (MCGMIL_DIAG_H0 ? 0 : rg.ob) + n;
     }
     int* ri = rinfo + kRowInfo * tid;
     ri[0] = hrow; ri[1] = t; ri[2] = n; ri[3] = rg.bag; ri[4] = rg.Nb;
@@ -977,7 +1047,7 @@ __device__ __forceinline__ RowState<E> region_row(const GateParams& p, const Reg
         const uint32_t tt = r / (uint32_t)rg.Nb;
         s.n = r - tt * (uint32_t)rg.Nb;
         s.t = (uint32_t)(p.t_base + rg.t0) + tt;
-        s.hsrc = H + (size_t)(rg.ob + (int)s.n) * p.ldh + kq * 8;
+        s.hsrc = H + (size_t)((MCGMIL_DIAG_H0 ? 0 : rg.ob) + (int)s.n) * p.ldh + kq * 8;
         s.inval = 0u;
     } else {
         s.n = 0u;
@@ -991,7 +1061,7 @@ __device__ __forceinline__ RowState<E> region_row(const GateParams& p, const Reg
 template <typename E, int PPW, int MAXC, bool ONE_CLASS>
 __device__ __forceinline__ void fused_region_tiles(const GateParams& p0, Region* srg, int ntiles,
                                                    E* Xs, float* red, float* zred, float* slg,
-                                                   float* szz) {
+                                                   float* szz, E* zw) {
     constexpr int BM = kPipeBM;
     constexpr int RT = BM / 16;
     constexpr int NJ = 2 * PPW;
@@ -1019,7 +1089,10 @@ __device__ __forceinline__ void fused_region_tiles(const GateParams& p0, Region*
         q = q < p0.P ? q : p0.P - 1;
         wA[j] = load_frag_buf<E>(wrs0, lane_b, (uint32_t)(2 * q + (j & 1)) * tile_bytes0);
     }
-    zA = load_frag_buf<E>(wrs0, lane_b, (uint32_t)(2 * p0.P) * tile_bytes0);
+    if constexpr (fused_zl<E>())   // the classifier fragments of all K steps, once per workgroup
+        load_classifier_lds<E>(wrs0, (uint32_t)(2 * p0.P) * tile_bytes0, KS0, zw);
+    else
+        zA = load_frag_buf<E>(wrs0, lane_b, (uint32_t)(2 * p0.P) * tile_bytes0);
     hB = load_raw(cur.hsrc + 32);
     {
         const uint4 o = philox4x32_10<true>((uint32_t)kq, cur.n, cur.t, cb, p0.k0, p0.k1);
@@ -1065,7 +1138,7 @@ __device__ __forceinline__ void fused_region_tiles(const GateParams& p0, Region*
             const int s1 = s + 1 < KS ? s + 1 : 0;
 #pragma unroll
             for (int j = 0; j < NJ; ++j) wn[j] = wfrag(wsoff[j] + (uint32_t)s1 * kStepBytes);
-            zn = wfrag(zsoff + (uint32_t)s1 * kStepBytes);
+            if constexpr (!fused_zl<E>()) zn = wfrag(zsoff + (uint32_t)s1 * kStepBytes);
             hn = load_raw(hs.hsrc + (size_t)hstep * 32);
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) {
@@ -1074,7 +1147,8 @@ __device__ __forceinline__ void fused_region_tiles(const GateParams& p0, Region*
                 for (int j = 0; j < NJ; ++j) acc[rt][j] = mma(w[j], x, acc[rt][j]);
             }
             const Frag<E> xz = load_frag(cs + (size_t)tid * 8);
-            zacc = mma(z, xz, zacc);
+            if constexpr (fused_zl<E>()) zacc = mma(load_frag(zw + (size_t)(s * 64 + lane) * 8), xz, zacc);
+            else zacc = mma(z, xz, zacc);
             {
                 const uint4 o = philox4x32_10<true>((uint32_t)(sstep * 4 + kq), ss.n, ss.t, cb, p.k0, p.k1);
                 store_dropped(h, o, p.thrx_f, ss.inval, ns + tid * 8);
@@ -1134,6 +1208,19 @@ __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GatePara
     float* szz = slg + CAP * MAXC;                                        // [CAP][C]
     float* sred = szz + CAP * MAXC;                                       // [2][16]
 
+#ifdef MCGMIL_DIAG_TPW   // diagnostic (timing only, no A/Y): TPW consecutive flat tiles per workgroup
+    for (int i = 0; i < MCGMIL_DIAG_TPW; ++i) {
+        const GateParams pt = reload_kernarg_params(p);
+        const long long R0 = ((long long)blockIdx.x * MCGMIL_DIAG_TPW + i) * BM;
+        if (R0 >= pt.total_samples) break;
+        int* ri = rinfo + (i & 1) * kRowInfo * BM;
+        fill_row_table<BM>(pt, R0, ri);
+        __syncthreads();
+        pipe_tile<E, PPW, MAXC, false, ONE_CLASS, MCGMIL_FUSED_EARLY_HV>(pt, R0, Xs, red, zred, ri,
+                                                                         pt.logits, pt.zz, 0);
+    }
+    return;
+#endif
 #if MCGMIL_DIAG & 64   // diagnostic (timing only): gate_pipe_kernel's work in this kernel's frame
     {
         const long long R0 = (long long)blockIdx.x * BM;
@@ -1155,8 +1242,18 @@ __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GatePara
     if (threadIdx.x == 0) *srg = rg;                 // read after the first tile's barrier
 #if MCGMIL_FUSED_PIPE
     __syncthreads();                                 // the region in LDS
-    if (ntiles > 0) fused_region_tiles<E, PPW, MAXC, ONE_CLASS>(p, srg, ntiles, Xs, red, zred, slg, szz);
+    if (ntiles > 0)
+        fused_region_tiles<E, PPW, MAXC, ONE_CLASS>(p, srg, ntiles, Xs, red, zred, slg, szz,
+                                                    reinterpret_cast<E*>(smem + fused_lds_bytes<E, MAXC>()));
 #else
+    E* zw = reinterpret_cast<E*>(smem + fused_lds_bytes<E, MAXC>());
+#if MCGMIL_FUSED_NEXT
+    TileLoads<E, 2 * PPW> tl;
+    const int srow_kq = (((int)threadIdx.x >> 6) * 16 + ((int)threadIdx.x & 15)) * 4 + (((int)threadIdx.x & 63) >> 4);
+#endif
+    if constexpr (fused_zl<E>())
+        load_classifier_lds<E>(make_rsrc(p.Wp, p.wp_bytes), (uint32_t)(2 * p.P) * (uint32_t)(p.L >> 5) * 512u *
+                                   (uint32_t)sizeof(E), p.L >> 5, zw);   // visible after tile 0's first barrier
     for (int i = 0; i < ntiles; ++i) {
         Region* qr = srg;
         asm volatile("" : "+v"(qr));
@@ -1176,9 +1273,18 @@ __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GatePara
         MCGMIL_STAMP(pt, 1);
         const Region r = *qr;
         const bool lds = r.Nb <= CAP && !MCGMIL_FUSED_GLOBAL;
-        pipe_tile<E, PPW, MAXC, false, ONE_CLASS, MCGMIL_FUSED_EARLY_HV>(pt, r.S + (long long)region_tile(r, i) * BM, Xs, red, zred, ri,
-                                                  lds ? slg : pt.logits, lds ? szz : pt.zz,
-                                                  lds ? r.S : 0);
+#if MCGMIL_FUSED_NEXT
+        // this thread's staging row of the next tile (this tile's again after the last one)
+        const E* next_hsrc =
+            region_row<E>(pt, r, region_tile(r, i + 1 < ntiles ? i + 1 : i), srow_kq >> 2, srow_kq & 3).hsrc;
+        pipe_tile<E, PPW, MAXC, false, ONE_CLASS, MCGMIL_FUSED_EARLY_HV, fused_zl<E>(), false, true>(
+            pt, r.S + (long long)region_tile(r, i) * BM, Xs, red, zred, ri, lds ? slg : pt.logits,
+            lds ? szz : pt.zz, lds ? r.S : 0, zw, &tl, i > 0, next_hsrc);
+#else
+        pipe_tile<E, PPW, MAXC, false, ONE_CLASS, MCGMIL_FUSED_EARLY_HV, fused_zl<E>(), false>(
+            pt, r.S + (long long)region_tile(r, i) * BM, Xs, red, zred, ri, lds ? slg : pt.logits,
+            lds ? szz : pt.zz, lds ? r.S : 0, zw);
+#endif
     }
 #endif
     __syncthreads();

@@ -22,6 +22,9 @@ for s in ${STEPS:-fused all cfg5 bench}; do
         cfg5) step bench_cfg5 600 python bench.py --workload cfg5 --steps 5 --warmup 2 --no-cpu-baseline ;;
         bench) step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
         bench16) step bench16 600 python bench.py --bags 16 --no-cpu-baseline ;;
+        cfg4) step bench_cfg4 600 python3 bench.py --workload cfg4 --steps 10 --warmup 3 --no-cpu-baseline ;;
+        cfg4two) step bench_cfg4_twokernel 600 env MCGMIL_FUSED=0 python3 bench.py --workload cfg4 --steps 10 --warmup 3 --no-cpu-baseline ;;
+        benchtwo) step bench_twokernel 600 env MCGMIL_FUSED=0 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
         abfused) step ab_fused 300 env MCGMIL_PROBE_LIBS="$(ls -1 abvar/*.so abvar2/*.so 2>/dev/null | paste -sd, -)" python -u scripts/probe_fused.py ;;
         abfused128) step ab_fused128 300 env PROBE_N=128 MCGMIL_PROBE_LIBS="$(ls -1 abvar/*.so abvar2/*.so 2>/dev/null | paste -sd, -)" python -u scripts/probe_fused.py ;;
         stamps) step stamps_flat 300 env PROBE_BAGS=128 python -u scripts/probe_stamps.py

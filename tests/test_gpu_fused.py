@@ -99,23 +99,34 @@ def test_fused_equals_two_kernel_path(cuda, case):
 
 
 def test_fused_auto_policy(cuda):
-    """MCGMIL_FUSED=auto takes the fused launch only for batches of >= 16,384 regions: 16 bags of
-    N=2048, T=100 (800 regions of two t-groups) do not, 512 bags (25,600) do. Unset: never."""
+    """MCGMIL_FUSED=auto (also the default, unset) takes the fused launch only for batches of
+    equal-size bags with >= 16,384 regions: 16 bags of N=2048, T=100 (800 regions of two t-groups)
+    do not, 512 bags (25,600, the bench's step) do, ragged batches do not. MCGMIL_FUSED=0: never."""
     from mcgmil import ops
     sd = synthetic.head_state_dict(0, C=2, shared=False)
     head = head_on(synthetic.head_arrays(sd, 2, False), cuda)
+    small = torch.zeros(16 * 2048, 512, device=cuda, dtype=torch.bfloat16)
+    small_offs = ops.bag_offsets_tensor([2048] * 16, cuda)
+    big = torch.zeros(512 * 2048, 512, device=cuda, dtype=torch.bfloat16)
+    big_offs = ops.bag_offsets_tensor([2048] * 512, cuda)
     with fused("auto"):
-        small = torch.zeros(16 * 2048, 512, device=cuda, dtype=torch.bfloat16)
-        assert regions(small, ops.bag_offsets_tensor([2048] * 16, cuda), head, 100) == 0
-        big = torch.zeros(512 * 2048, 512, device=cuda, dtype=torch.bfloat16)
-        big_offs = ops.bag_offsets_tensor([2048] * 512, cuda)
+        assert regions(small, small_offs, head, 100) == 0
         assert regions(big, big_offs, head, 100) == 512 * 50
     old = os.environ.pop("MCGMIL_FUSED", None)
     try:
-        assert regions(big, big_offs, head, 100) == 0
+        assert regions(small, small_offs, head, 100) == 0
+        assert regions(big, big_offs, head, 100) == 512 * 50
     finally:
         if old is not None:
             os.environ["MCGMIL_FUSED"] = old
+    with fused("0"):
+        assert regions(big, big_offs, head, 100) == 0
+    # ragged batches (config 4) stay on the two-kernel path under auto, however many regions
+    ragged_offs = ops.bag_offsets_tensor([2047, 2049] * 256, cuda)
+    with fused("auto"):
+        assert regions(big, ragged_offs, head, 100) == 0
+    with fused("1"):
+        assert regions(big, ragged_offs, head, 100) > 16384
 
 
 from test_gpu_parity import BF16_CASES, FP32_CASES, TOL32, TOL_BF16_IN, compare, run  # noqa: E402
