@@ -632,25 +632,14 @@ __device__ __forceinline__ void load_classifier_lds(__amdgpu_buffer_rsrc_t wrs, 
             f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, (uint32_t)i * 8u * (uint32_t)sizeof(E), zsoff, 0));
 }
 
-// A tile's prologue loads (H of steps 0 and 1 of the thread's staging row, step-0 weights),
-// issued by the PREVIOUS tile of the same workgroup right after its K loop (pipe_tile's NEXT
-// mode), so they land under that tile's epilogue instead of in this tile's prologue.
-template <typename E, int NJ>
-struct TileLoads {
-    Raw<E> h0, h1;
-    Frag<E> w[NJ];
-};
-
 // One 128-row tile of the flattened (bag, t, n) space, rows R0 .. R0+127, whose row table is
 // already in `rinfo` (and visible: the caller's barrier). Scores go to lg_out / z_out at row
 // R0 + r - obase. LDS: Xs [2][SLOT] staging slots, red / zred the cross-wave reductions.
 template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS, bool EARLY_HV = true,
-          bool ZL = false, bool ZLOAD = true, bool NEXT = false>
+          bool ZL = false, bool ZLOAD = true>
 __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* Xs, float* red,
                                           float* zred, const int* rinfo, float* lg_out,
-                                          float* z_out, long long obase, E* zw = nullptr,
-                                          TileLoads<E, 2 * PPW>* tl = nullptr, bool have_tl = false,
-                                          const E* next_hsrc = nullptr) {
+                                          float* z_out, long long obase, E* zw = nullptr) {
     constexpr int BM = kPipeBM;
     constexpr int RT = BM / 16;                     // 8 row tiles = 8 waves
     constexpr int NJ = 2 * PPW;
@@ -780,17 +769,10 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
     // prologue: stage step 0, load the weights of step 0 and H of step 1
     Frag<E> wA[NJ], wB[NJ], zA, zB;
     Raw<E> hA, hB;
-    if (NEXT && have_tl) {            // issued by the previous tile (NEXT mode), under its epilogue
-        hA = tl->h0;
-        hB = tl->h1;
+    hA = load_raw(hsrc);
+    hB = load_raw(hsrc + 32);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) wA[j] = tl->w[j];
-    } else {
-        hA = load_raw(hsrc);
-        hB = load_raw(hsrc + 32);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) wA[j] = wfrag(wsoff[j]);
-    }
+    for (int j = 0; j < NJ; ++j) wA[j] = wfrag(wsoff[j]);
     if constexpr (ZL) {
         // ZL: the classifier tile's fragments of all K steps sit in LDS (ZLOAD: loaded here, by
         // this tile; else by the caller, once), so the K loop reads them with one ds_read per
@@ -822,12 +804,6 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
         kstep(s + 1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB);
     }
     MCGMIL_STAMP(p, 3);
-    if constexpr (NEXT) {             // the next tile's prologue loads, in flight under the epilogue
-        tl->h0 = load_raw(next_hsrc);
-        tl->h1 = load_raw(next_hsrc + 32);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) tl->w[j] = wfrag(wsoff[j]);
-    }
 
     float part[MAXC][RT];
 #pragma unroll
@@ -893,9 +869,6 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
 #endif
 #ifndef MCGMIL_FUSED_NMAJOR
 #define MCGMIL_FUSED_NMAJOR 1
-#endif
-#ifndef MCGMIL_FUSED_NEXT
-#define MCGMIL_FUSED_NEXT 0        // 1: a tile issues the next tile's prologue loads under its epilogue (spills: 160 B)
 #endif
 #ifndef MCGMIL_FUSED_CAP
 #define MCGMIL_FUSED_CAP 4096      // rows of one region's logits in LDS (C <= 2)
@@ -1247,10 +1220,6 @@ __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GatePara
                                                     reinterpret_cast<E*>(smem + fused_lds_bytes<E, MAXC>()));
 #else
     E* zw = reinterpret_cast<E*>(smem + fused_lds_bytes<E, MAXC>());
-#if MCGMIL_FUSED_NEXT
-    TileLoads<E, 2 * PPW> tl;
-    const int srow_kq = (((int)threadIdx.x >> 6) * 16 + ((int)threadIdx.x & 15)) * 4 + (((int)threadIdx.x & 63) >> 4);
-#endif
     if constexpr (fused_zl<E>())
         load_classifier_lds<E>(make_rsrc(p.Wp, p.wp_bytes), (uint32_t)(2 * p.P) * (uint32_t)(p.L >> 5) * 512u *
                                    (uint32_t)sizeof(E), p.L >> 5, zw);   // visible after tile 0's first barrier
@@ -1273,18 +1242,9 @@ __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GatePara
         MCGMIL_STAMP(pt, 1);
         const Region r = *qr;
         const bool lds = r.Nb <= CAP && !MCGMIL_FUSED_GLOBAL;
-#if MCGMIL_FUSED_NEXT
-        // this thread's staging row of the next tile (this tile's again after the last one)
-        const E* next_hsrc =
-            region_row<E>(pt, r, region_tile(r, i + 1 < ntiles ? i + 1 : i), srow_kq >> 2, srow_kq & 3).hsrc;
-        pipe_tile<E, PPW, MAXC, false, ONE_CLASS, MCGMIL_FUSED_EARLY_HV, fused_zl<E>(), false, true>(
-            pt, r.S + (long long)region_tile(r, i) * BM, Xs, red, zred, ri, lds ? slg : pt.logits,
-            lds ? szz : pt.zz, lds ? r.S : 0, zw, &tl, i > 0, next_hsrc);
-#else
         pipe_tile<E, PPW, MAXC, false, ONE_CLASS, MCGMIL_FUSED_EARLY_HV, fused_zl<E>(), false>(
             pt, r.S + (long long)region_tile(r, i) * BM, Xs, red, zred, ri, lds ? slg : pt.logits,
             lds ? szz : pt.zz, lds ? r.S : 0, zw);
-#endif
     }
 #endif
     __syncthreads();
