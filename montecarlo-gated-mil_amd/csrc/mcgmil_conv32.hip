@@ -1,0 +1,242 @@
+// fp32 convolution for the backbone at the reference precision (config 5's fp32 line): an implicit
+// GEMM on v_mfma_f32_16x16x4_f32 with fp32 operands and fp32 accumulation, NHWC in and out.
+// Reference: torch.nn.Conv2d.forward in fp32 (model.py:166-179, the ResNet feature extractor).
+//
+// GEMM view: rows = output channels (the A operand, weights), columns = output pixels (the B
+// operand, im2col of x), K = (kh, kw, ci) in steps of 16 input channels of one tap. A workgroup of
+// 4 waves computes BN_CO x BM_PX = 128 x 128 (or 64 x 256 when Cout = 64), each wave a 64 x 64
+// block = 4 x 4 tiles of 16 x 16 (64 accumulator VGPRs). Per 16-deep K step a wave issues 64 MFMAs
+// (32 cycles each on its SIMD) against 32 ds_read_b32 of LDS fragments, so the matrix pipe, not
+// LDS or memory, sets the pace. Staging: the next K step's A and B pieces are loaded into
+// registers while the current one computes, then written to the other of two LDS stages.
+//
+// LDS fragments: lane l of a 16x16x4 fp32 MFMA holds A[row l&15][k l>>4] and B[k l>>4][col l&15];
+// the stages are k-major rows ([16][BN_CO + 16] and [16][BM_PX + 16] floats), so the 16 lanes of
+// one k read 16 consecutive words and the 16-word row pad puts the next k on the next 16 banks:
+// every ds_read_b32 is conflict-free. The C layout gives a lane 4 consecutive output channels of
+// one pixel: one 16-byte store per tile.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mcgmil.h"
+#include "../../include/mcgmil_features.h"
+#include "mcgmil_error.h"
+
+namespace {
+
+using mcgmil_detail::fail;
+using mcgmil_detail::hip_fail;
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+struct Conv32Geom {
+    int N, H, W, Cin, Cout, KH, KW, stride, pad, OH, OW;
+    long long P;          // N * OH * OW output pixels
+    int KS;               // K steps: KH * KW * Cin / 16
+};
+
+constexpr int kK = 16;    // K step (input channels of one tap)
+constexpr int kPad = 16;  // LDS row pad (words)
+
+template <int WCO, int WPX>
+struct Tile {
+    static constexpr int BN_CO = 64 * WCO, BM_PX = 64 * WPX;
+    static constexpr int AS = BN_CO + kPad, BS = BM_PX + kPad;              // row strides (floats)
+    static constexpr int STAGE = kK * (AS + BS);                             // floats per stage
+    static constexpr int A4 = kK * BN_CO / 4 / 256, B4 = kK * BM_PX / 4 / 256;   // float4 per thread
+};
+
+template <int WCO, int WPX>
+__global__ __launch_bounds__(256) void conv32_kernel(const Conv32Geom g, const float* __restrict__ x,
+                                                     const float* __restrict__ w, float* __restrict__ y) {
+    using T = Tile<WCO, WPX>;
+    extern __shared__ __attribute__((aligned(16))) float smem32[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wco = wave % WCO, wpx = wave / WCO;
+    const long long px0 = (long long)blockIdx.x * T::BM_PX;
+    const int co0 = blockIdx.y * T::BN_CO;
+
+    // B staging: every thread owns pixel tid % BM_PX of the block and some of its 4 ci quads
+    const int bpx = tid % T::BM_PX;
+    const int bq0 = tid / T::BM_PX;               // first ci quad; quads bq0 + (256 / BM_PX) r
+    constexpr int QSTEP = 256 / T::BM_PX;
+    const long long p = px0 + bpx;
+    const bool pvalid = p < g.P;
+    int n = 0, oh = 0, ow = 0;
+    if (pvalid) {
+        const long long ohw = (long long)g.OH * g.OW;
+        n = (int)(p / ohw);
+        const int r = (int)(p - (long long)n * ohw);
+        oh = r / g.OW;
+        ow = r - oh * g.OW;
+    }
+    const int ih0 = oh * g.stride - g.pad, iw0 = ow * g.stride - g.pad;
+    const float* xn = x + (long long)n * g.H * g.W * g.Cin;
+    const int cchunks = g.Cin / kK;
+
+    f32x4 ra[T::A4], rb[T::B4];
+    auto load = [&](int ks) {
+        // A: packed weights [KS][16][Cout], rows k of this K step, columns co0 .. co0 + BN_CO
+        const float* wk = w + (long long)ks * kK * g.Cout + co0;
+#pragma unroll
+        for (int r = 0; r < T::A4; ++r) {
+            const int f = tid + 256 * r;
+            const int k = f / (T::BN_CO / 4), c4 = f % (T::BN_CO / 4);
+            ra[r] = *reinterpret_cast<const f32x4*>(wk + (long long)k * g.Cout + 4 * c4);
+        }
+        // B: x[n, ih, iw, ci0 + 4q .. +3] of this thread's pixel (zero outside the image)
+        const int tap = ks / cchunks, ci0 = (ks - tap * cchunks) * kK;
+        const int kh = tap / g.KW, kw = tap - kh * g.KW;
+        const int ih = ih0 + kh, iw = iw0 + kw;
+        const bool in = pvalid && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        const float* src = xn + ((long long)(in ? ih : 0) * g.W + (in ? iw : 0)) * g.Cin + ci0;
+#pragma unroll
+        for (int r = 0; r < T::B4; ++r) {
+            const int q = bq0 + QSTEP * r;
+            rb[r] = in ? *reinterpret_cast<const f32x4*>(src + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto store = [&](float* st) {
+        float* As = st;
+        float* Bs = st + kK * T::AS;
+#pragma unroll
+        for (int r = 0; r < T::A4; ++r) {
+            const int f = tid + 256 * r;
+            const int k = f / (T::BN_CO / 4), c4 = f % (T::BN_CO / 4);
+            *reinterpret_cast<f32x4*>(As + k * T::AS + 4 * c4) = ra[r];
+        }
+#pragma unroll
+        for (int r = 0; r < T::B4; ++r) {
+            const int q = bq0 + QSTEP * r;
+            Bs[(4 * q + 0) * T::BS + bpx] = rb[r].x;
+            Bs[(4 * q + 1) * T::BS + bpx] = rb[r].y;
+            Bs[(4 * q + 2) * T::BS + bpx] = rb[r].z;
+            Bs[(4 * q + 3) * T::BS + bpx] = rb[r].w;
+        }
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int kl = lane >> 4, cl = lane & 15;
+    load(0);
+    store(smem32);
+    __syncthreads();
+    for (int ks = 0; ks < g.KS; ++ks) {
+        const float* st = smem32 + (ks & 1) * T::STAGE;
+        const float* As = st + wco * 64 + cl;
+        const float* Bs = st + kK * T::AS + wpx * 64 + cl;
+        if (ks + 1 < g.KS) load(ks + 1);
+#pragma unroll
+        for (int s = 0; s < kK / 4; ++s) {
+            const int k = 4 * s + kl;
+            float a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = As[k * T::AS + 16 * i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = Bs[k * T::BS + 16 * j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        if (ks + 1 < g.KS) store(smem32 + ((ks + 1) & 1) * T::STAGE);
+        __syncthreads();
+    }
+
+    // D tile (i, j): lane holds channels co0 + wco*64 + 16 i + 4 (lane >> 4) + v of pixel
+    // px0 + wpx*64 + 16 j + (lane & 15)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const long long pp = px0 + wpx * 64 + 16 * j + cl;
+        if (pp >= g.P) continue;
+        float* yp = y + pp * g.Cout + co0 + wco * 64 + 4 * kl;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<f32x4*>(yp + 16 * i) = acc[i][j];
+    }
+}
+
+// torch layout [Cout, Cin, KH, KW] fp32 -> [KS][16][Cout] with K step ks = (kh*KW + kw)*(Cin/16) + ci/16
+__global__ void pack_conv32_kernel(const float* w, int Cout, int Cin, int KH, int KW, float* out) {
+    const long long total = (long long)Cout * Cin * KH * KW;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int co = (int)(i % Cout);
+        long long r = i / Cout;                    // r = ks * 16 + k
+        const int k = (int)(r % kK);
+        const long long ks = r / kK;
+        const int cchunks = Cin / kK;
+        const int tap = (int)(ks / cchunks), ci = (int)(ks % cchunks) * kK + k;
+        const int kh = tap / KW, kw = tap % KW;
+        out[i] = w[(((long long)co * Cin + ci) * KH + kh) * KW + kw];
+    }
+}
+
+int validate32(const mcgmil_conv_args* a, Conv32Geom* g) {
+    if (!a) return fail(MCGMIL_E_INVALID, "args is NULL");
+    if (a->batch < 1 || a->height < 1 || a->width < 1)
+        return fail(MCGMIL_E_INVALID, "batch, height and width must be >= 1");
+    if (a->in_channels < kK || a->in_channels % kK != 0 || a->out_channels < 64 || a->out_channels % 64 != 0)
+        return fail(MCGMIL_E_UNSUPPORTED, "fp32 convolution: in_channels a multiple of 16, out_channels of 64");
+    if (a->kernel_h < 1 || a->kernel_w < 1 || a->kernel_h > 7 || a->kernel_w > 7)
+        return fail(MCGMIL_E_UNSUPPORTED, "kernel size must be in 1..7");
+    if (a->stride < 1 || a->pad < 0 || a->pad > 64) return fail(MCGMIL_E_INVALID, "stride >= 1 and 0 <= pad <= 64");
+    if (a->in_ab || a->stats) return fail(MCGMIL_E_UNSUPPORTED, "fp32 convolution: no in_ab / stats");
+    const long long oh = ((long long)a->height + 2 * a->pad - a->kernel_h) / a->stride + 1;
+    const long long ow = ((long long)a->width + 2 * a->pad - a->kernel_w) / a->stride + 1;
+    if (oh < 1 || ow < 1) return fail(MCGMIL_E_INVALID, "the kernel does not fit the padded input");
+    const long long P = (long long)a->batch * oh * ow;
+    if (P >= (1ll << 31) - 256) return fail(MCGMIL_E_UNSUPPORTED, "too many output pixels");
+    if (g) {
+        g->N = a->batch; g->H = a->height; g->W = a->width; g->Cin = a->in_channels;
+        g->Cout = a->out_channels; g->KH = a->kernel_h; g->KW = a->kernel_w;
+        g->stride = a->stride; g->pad = a->pad; g->OH = (int)oh; g->OW = (int)ow; g->P = P;
+        g->KS = a->kernel_h * a->kernel_w * (a->in_channels / kK);
+    }
+    return MCGMIL_OK;
+}
+
+template <int WCO, int WPX>
+int launch32(const Conv32Geom& g, const float* x, const float* w, float* y, hipStream_t s) {
+    using T = Tile<WCO, WPX>;
+    const size_t lds = (size_t)2 * T::STAGE * sizeof(float);
+    dim3 grid((unsigned)((g.P + T::BM_PX - 1) / T::BM_PX), (unsigned)(g.Cout / T::BN_CO));
+    hipLaunchKernelGGL((conv32_kernel<WCO, WPX>), grid, dim3(256), lds, s, g, x, w, y);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "conv32_kernel launch");
+}
+
+}  // namespace
+
+extern "C" {
+
+int mcgmil_pack_conv_weights_f32(const mcgmil_conv_args* a, const void* weight, void* packed, void* stream) {
+    if (int rc = validate32(a, nullptr)) return rc;
+    if (!weight || !packed) return fail(MCGMIL_E_INVALID, "NULL weight or packed pointer");
+    const long long total = (long long)a->out_channels * a->in_channels * a->kernel_h * a->kernel_w;
+    const unsigned blocks = (unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(pack_conv32_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       static_cast<const float*>(weight), a->out_channels, a->in_channels, a->kernel_h,
+                       a->kernel_w, static_cast<float*>(packed));
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "pack_conv32_kernel launch");
+}
+
+int mcgmil_conv2d_f32(const mcgmil_conv_args* a, void* stream) {
+    Conv32Geom g;
+    if (int rc = validate32(a, &g)) return rc;
+    if (!a->x || !a->w || !a->y) return fail(MCGMIL_E_INVALID, "NULL x, w or y");
+    if (((uintptr_t)a->x | (uintptr_t)a->w | (uintptr_t)a->y) & 15u)
+        return fail(MCGMIL_E_ALIGN, "x, w and y must be 16-byte aligned");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const float* x = static_cast<const float*>(a->x);
+    const float* w = static_cast<const float*>(a->w);
+    float* y = static_cast<float*>(a->y);
+    return g.Cout % 128 == 0 ? launch32<2, 2>(g, x, w, y, s) : launch32<1, 4>(g, x, w, y, s);
+}
+
+}  // extern "C"

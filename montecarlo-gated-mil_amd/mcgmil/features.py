@@ -175,6 +175,75 @@ def conv2d(conv: nn.Conv2d, x: torch.Tensor, stats: bool = False,
     return (y, part) if stats else y
 
 
+def conv32_enabled() -> bool:
+    """MCGMIL_NATIVE_CONV32=0 keeps fp32 convolutions on the torch layers (MIOpen)."""
+    return os.environ.get("MCGMIL_NATIVE_CONV32", "1") != "0" and conv_enabled()
+
+
+def conv32_fusable(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """A CUDA channels-last fp32 activation (no autocast) and a convolution the fp32 kernel
+    implements (mcgmil_conv2d_f32: in_channels % 16, out_channels % 64, kernel <= 7), no autograd."""
+    if not (conv32_enabled() and isinstance(conv, nn.Conv2d) and x.is_cuda and x.dim() == 4):
+        return False
+    if x.dtype != torch.float32 or torch.is_autocast_enabled("cuda"):
+        return False
+    if conv.groups != 1 or conv.bias is not None or conv.padding_mode != "zeros":
+        return False
+    if _square(conv.dilation) != 1 or _square(conv.stride) is None or \
+            not isinstance(conv.padding, tuple) or _square(conv.padding) is None:
+        return False
+    kh, kw = conv.kernel_size
+    if not (1 <= kh <= 7 and 1 <= kw <= 7):
+        return False
+    if conv.in_channels % 16 or conv.out_channels % 64 or x.shape[1] != conv.in_channels:
+        return False
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        return False
+    if torch.is_grad_enabled() and (x.requires_grad or conv.weight.requires_grad):
+        return False
+    oh = (x.shape[2] + 2 * _square(conv.padding) - kh) // _square(conv.stride) + 1
+    ow = (x.shape[3] + 2 * _square(conv.padding) - kw) // _square(conv.stride) + 1
+    return x.shape[0] * oh * ow < 2 ** 31 - 256
+
+
+def packed_conv_weight_f32(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """The fp32 weight in mcgmil_conv2d_f32's packed layout, cached on the module until it changes."""
+    w = conv.weight.detach()
+    key = (w.data_ptr(), w._version, w.dtype, x.device, "f32")
+    cached = getattr(conv, "_mcgmil_packed32", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    L = _lib.load()
+    w32 = w.to(device=x.device, dtype=torch.float32).contiguous()
+    packed = torch.empty(w32.numel(), dtype=torch.float32, device=x.device)
+    a = _conv_args(conv, x)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    _lib.check(L.mcgmil_pack_conv_weights_f32(ctypes.byref(a), ctypes.c_void_p(w32.data_ptr()),
+                                              ctypes.c_void_p(packed.data_ptr()), stream),
+               "mcgmil_pack_conv_weights_f32")
+    conv._mcgmil_packed32 = (key, packed)
+    return packed
+
+
+def conv2d_f32(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """conv(x) in fp32 on the MFMA kernel (fp32 operands and accumulation) for a channels-last fp32
+    activation (see conv32_fusable); returns a channels-last fp32 tensor."""
+    if not conv32_fusable(conv, x):
+        raise ValueError("conv2d_f32 needs a CUDA channels-last fp32 activation and a bias-free groups=1 "
+                         "convolution with in_channels % 16 == 0, out_channels % 64 == 0 (conv32_fusable)")
+    L = _lib.load()
+    a = _conv_args(conv, x)
+    oh = (a.height + 2 * a.pad - a.kernel_h) // a.stride + 1
+    ow = (a.width + 2 * a.pad - a.kernel_w) // a.stride + 1
+    y = torch.empty((a.batch, a.out_channels, oh, ow), dtype=torch.float32, device=x.device,
+                    memory_format=torch.channels_last)
+    w = packed_conv_weight_f32(conv, x)
+    a.x, a.w, a.y = (ctypes.c_void_p(t.data_ptr()) for t in (x, w, y))
+    stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    _lib.check(L.mcgmil_conv2d_f32(ctypes.byref(a), stream), "mcgmil_conv2d_f32")
+    return y
+
+
 def torch_conv(layer: nn.Module, x: torch.Tensor) -> torch.Tensor:
     """The torch layer, with fp32 convolutions on the GPU split along the batch so that no call's
     input or output reaches 2^31 bytes (MCGMIL_FP32_CONV_CHUNK=0: unsplit). On some MI355X boxes
@@ -197,9 +266,12 @@ def torch_conv(layer: nn.Module, x: torch.Tensor) -> torch.Tensor:
 
 
 def run_conv(layer: nn.Module, x: torch.Tensor) -> torch.Tensor:
-    """The backbone's convolution: the MFMA kernel when `conv_fusable`, else the torch layer."""
+    """The backbone's convolution: the bf16 MFMA kernel when `conv_fusable`, the fp32 one when
+    `conv32_fusable`, else the torch layer."""
     if isinstance(layer, nn.Conv2d) and conv_fusable(layer, x):
         return conv2d(layer, x)
+    if isinstance(layer, nn.Conv2d) and conv32_fusable(layer, x):
+        return conv2d_f32(layer, x)
     return torch_conv(layer, x)
 
 
