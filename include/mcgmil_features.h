@@ -163,8 +163,11 @@ int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream);
 /* The same convolution in fp32 (the reference precision: fp32 operands, fp32 accumulation on
  * v_mfma_f32_16x16x4_f32): x [batch, height, width, in_channels] fp32 NHWC, y fp32 NHWC, w the
  * packed fp32 weight made by mcgmil_pack_conv_weights_f32 from the torch layout [out, in, kh, kw]
- * fp32 (out * kh * kw * in floats). in_channels a multiple of 16, out_channels of 64, kernel
- * 1..7; no in_ab, no stats (MCGMIL_E_UNSUPPORTED). 16-byte aligned pointers. */
+ * fp32 (mcgmil_conv_packed_size_f32 floats). out_channels a multiple of 64, kernel 1..7, and
+ * in_channels a multiple of 16 or kernel_h * kernel_w * in_channels <= 1024 (the 3-channel stem,
+ * one 4-byte gather per element); no in_ab, no stats (MCGMIL_E_UNSUPPORTED). 16-byte aligned
+ * pointers. */
+int mcgmil_conv_packed_size_f32(const mcgmil_conv_args* a, size_t* floats);
 int mcgmil_pack_conv_weights_f32(const mcgmil_conv_args* a, const void* weight, void* packed, void* stream);
 int mcgmil_conv2d_f32(const mcgmil_conv_args* a, void* stream);
 int mcgmil_bn_workspace_size(const mcgmil_bn_args* a, size_t* bytes);

@@ -32,8 +32,14 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 struct Conv32Geom {
     int N, H, W, Cin, Cout, KH, KW, stride, pad, OH, OW;
     long long P;          // N * OH * OW output pixels
-    int KS;               // K steps: KH * KW * Cin / 16
+    int KS;               // K steps of 16: KH * KW * Cin / 16, or ceil(KH * KW * Cin / 16) (gather)
+    int Ktot;             // KH * KW * Cin
 };
+
+// Gather mode (in_channels not a multiple of 16: the 3-channel stem): K is the flattened
+// (kh, kw, ci) of the NHWC window, zero-padded to whole steps, and every B element is its own
+// 4-byte load through a per-workgroup LDS table of k -> (offset in the window, kh, kw).
+constexpr int kMaxGatherK = 1024;
 
 constexpr int kK = 16;    // K step (input channels of one tap)
 constexpr int kPad = 16;  // LDS row pad (words)
@@ -46,11 +52,28 @@ struct Tile {
     static constexpr int A4 = kK * BN_CO / 4 / 256, B4 = kK * BM_PX / 4 / 256;   // float4 per thread
 };
 
-template <int WCO, int WPX>
+template <int WCO, int WPX, bool GATHER>
 __global__ __launch_bounds__(256) void conv32_kernel(const Conv32Geom g, const float* __restrict__ x,
                                                      const float* __restrict__ w, float* __restrict__ y) {
     using T = Tile<WCO, WPX>;
     extern __shared__ __attribute__((aligned(16))) float smem32[];
+    // gather table after the two stages: k -> window offset (floats) and kh | kw << 8
+    int* gtab = reinterpret_cast<int*>(smem32 + 2 * T::STAGE);
+    if constexpr (GATHER) {
+        const int kpad = g.KS * kK;
+        for (int k = threadIdx.x; k < kpad; k += 256) {
+            int off = -1, hw = 0;
+            if (k < g.Ktot) {
+                const int tap = k / g.Cin, ci = k - tap * g.Cin;
+                const int kh = tap / g.KW, kw = tap - kh * g.KW;
+                off = (kh * g.W + kw) * g.Cin + ci;
+                hw = kh | (kw << 8);
+            }
+            gtab[2 * k] = off;
+            gtab[2 * k + 1] = hw;
+        }
+        __syncthreads();
+    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wco = wave % WCO, wpx = wave / WCO;
     const long long px0 = (long long)blockIdx.x * T::BM_PX;
@@ -72,7 +95,7 @@ __global__ __launch_bounds__(256) void conv32_kernel(const Conv32Geom g, const f
     }
     const int ih0 = oh * g.stride - g.pad, iw0 = ow * g.stride - g.pad;
     const float* xn = x + (long long)n * g.H * g.W * g.Cin;
-    const int cchunks = g.Cin / kK;
+    const int cchunks = g.Cin / kK > 0 ? g.Cin / kK : 1;
 
     f32x4 ra[T::A4], rb[T::B4];
     auto load = [&](int ks) {
@@ -83,6 +106,24 @@ __global__ __launch_bounds__(256) void conv32_kernel(const Conv32Geom g, const f
             const int f = tid + 256 * r;
             const int k = f / (T::BN_CO / 4), c4 = f % (T::BN_CO / 4);
             ra[r] = *reinterpret_cast<const f32x4*>(wk + (long long)k * g.Cout + 4 * c4);
+        }
+        if constexpr (GATHER) {   // one 4-byte load per element, window offsets from the table
+            const float* base = xn + ((long long)ih0 * g.W + iw0) * g.Cin;
+#pragma unroll
+            for (int r = 0; r < T::B4; ++r) {
+                const int q = bq0 + QSTEP * r;
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int k = ks * kK + 4 * q + e;
+                    const int off = gtab[2 * k], hw = gtab[2 * k + 1];
+                    const int ih = ih0 + (hw & 255), iw = iw0 + (hw >> 8);
+                    const bool in = pvalid && off >= 0 && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+                    v[e] = in ? base[off] : 0.f;
+                }
+                rb[r] = f32x4{v[0], v[1], v[2], v[3]};
+            }
+            return;
         }
         // B: x[n, ih, iw, ci0 + 4q .. +3] of this thread's pixel (zero outside the image)
         const int tap = ks / cchunks, ci0 = (ks - tap * cchunks) * kK;
@@ -160,17 +201,28 @@ __global__ __launch_bounds__(256) void conv32_kernel(const Conv32Geom g, const f
     }
 }
 
-// torch layout [Cout, Cin, KH, KW] fp32 -> [KS][16][Cout] with K step ks = (kh*KW + kw)*(Cin/16) + ci/16
-__global__ void pack_conv32_kernel(const float* w, int Cout, int Cin, int KH, int KW, float* out) {
-    const long long total = (long long)Cout * Cin * KH * KW;
+// torch layout [Cout, Cin, KH, KW] fp32 -> [KS][16][Cout]: row r = ks * 16 + k of K = (kh, kw, ci)
+// (Cin % 16 == 0: K step ks = (kh*KW + kw)*(Cin/16) + ci/16; gather mode: r = (kh*KW + kw)*Cin + ci
+// itself, zero rows past KH*KW*Cin)
+__global__ void pack_conv32_kernel(const float* w, int Cout, int Cin, int KH, int KW, int KS, float* out) {
+    const long long total = (long long)KS * kK * Cout;
+    const bool gather = Cin % kK != 0;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (long long)gridDim.x * blockDim.x) {
         const int co = (int)(i % Cout);
-        long long r = i / Cout;                    // r = ks * 16 + k
-        const int k = (int)(r % kK);
-        const long long ks = r / kK;
-        const int cchunks = Cin / kK;
-        const int tap = (int)(ks / cchunks), ci = (int)(ks % cchunks) * kK + k;
+        const long long r = i / Cout;
+        int tap, ci;
+        if (gather) {
+            if (r >= (long long)KH * KW * Cin) { out[i] = 0.f; continue; }
+            tap = (int)(r / Cin);
+            ci = (int)(r % Cin);
+        } else {
+            const int k = (int)(r % kK);
+            const long long ks = r / kK;
+            const int cchunks = Cin / kK;
+            tap = (int)(ks / cchunks);
+            ci = (int)(ks % cchunks) * kK + k;
+        }
         const int kh = tap / KW, kw = tap % KW;
         out[i] = w[(((long long)co * Cin + ci) * KH + kh) * KW + kw];
     }
@@ -180,8 +232,12 @@ int validate32(const mcgmil_conv_args* a, Conv32Geom* g) {
     if (!a) return fail(MCGMIL_E_INVALID, "args is NULL");
     if (a->batch < 1 || a->height < 1 || a->width < 1)
         return fail(MCGMIL_E_INVALID, "batch, height and width must be >= 1");
-    if (a->in_channels < kK || a->in_channels % kK != 0 || a->out_channels < 64 || a->out_channels % 64 != 0)
-        return fail(MCGMIL_E_UNSUPPORTED, "fp32 convolution: in_channels a multiple of 16, out_channels of 64");
+    if (a->in_channels < 1 || a->out_channels < 64 || a->out_channels % 64 != 0)
+        return fail(MCGMIL_E_UNSUPPORTED, "fp32 convolution: out_channels a multiple of 64");
+    if (a->in_channels % kK != 0 &&
+        (long long)a->kernel_h * a->kernel_w * a->in_channels > kMaxGatherK)
+        return fail(MCGMIL_E_UNSUPPORTED, "fp32 convolution: in_channels not a multiple of 16 needs "
+                                          "kernel_h * kernel_w * in_channels <= 1024");
     if (a->kernel_h < 1 || a->kernel_w < 1 || a->kernel_h > 7 || a->kernel_w > 7)
         return fail(MCGMIL_E_UNSUPPORTED, "kernel size must be in 1..7");
     if (a->stride < 1 || a->pad < 0 || a->pad > 64) return fail(MCGMIL_E_INVALID, "stride >= 1 and 0 <= pad <= 64");
@@ -195,17 +251,18 @@ int validate32(const mcgmil_conv_args* a, Conv32Geom* g) {
         g->N = a->batch; g->H = a->height; g->W = a->width; g->Cin = a->in_channels;
         g->Cout = a->out_channels; g->KH = a->kernel_h; g->KW = a->kernel_w;
         g->stride = a->stride; g->pad = a->pad; g->OH = (int)oh; g->OW = (int)ow; g->P = P;
-        g->KS = a->kernel_h * a->kernel_w * (a->in_channels / kK);
+        g->Ktot = a->kernel_h * a->kernel_w * a->in_channels;
+        g->KS = (g->Ktot + kK - 1) / kK;
     }
     return MCGMIL_OK;
 }
 
-template <int WCO, int WPX>
+template <int WCO, int WPX, bool GATHER>
 int launch32(const Conv32Geom& g, const float* x, const float* w, float* y, hipStream_t s) {
     using T = Tile<WCO, WPX>;
-    const size_t lds = (size_t)2 * T::STAGE * sizeof(float);
+    const size_t lds = (size_t)2 * T::STAGE * sizeof(float) + (GATHER ? (size_t)g.KS * kK * 8 : 0);
     dim3 grid((unsigned)((g.P + T::BM_PX - 1) / T::BM_PX), (unsigned)(g.Cout / T::BN_CO));
-    hipLaunchKernelGGL((conv32_kernel<WCO, WPX>), grid, dim3(256), lds, s, g, x, w, y);
+    hipLaunchKernelGGL((conv32_kernel<WCO, WPX, GATHER>), grid, dim3(256), lds, s, g, x, w, y);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "conv32_kernel launch");
 }
@@ -217,13 +274,23 @@ extern "C" {
 int mcgmil_pack_conv_weights_f32(const mcgmil_conv_args* a, const void* weight, void* packed, void* stream) {
     if (int rc = validate32(a, nullptr)) return rc;
     if (!weight || !packed) return fail(MCGMIL_E_INVALID, "NULL weight or packed pointer");
-    const long long total = (long long)a->out_channels * a->in_channels * a->kernel_h * a->kernel_w;
+    Conv32Geom g;
+    validate32(a, &g);
+    const long long total = (long long)g.KS * kK * a->out_channels;
     const unsigned blocks = (unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
     hipLaunchKernelGGL(pack_conv32_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                        static_cast<const float*>(weight), a->out_channels, a->in_channels, a->kernel_h,
-                       a->kernel_w, static_cast<float*>(packed));
+                       a->kernel_w, g.KS, static_cast<float*>(packed));
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "pack_conv32_kernel launch");
+}
+
+int mcgmil_conv_packed_size_f32(const mcgmil_conv_args* a, size_t* floats) {
+    Conv32Geom g;
+    if (int rc = validate32(a, &g)) return rc;
+    if (!floats) return fail(MCGMIL_E_INVALID, "floats is NULL");
+    *floats = (size_t)g.KS * kK * a->out_channels;
+    return MCGMIL_OK;
 }
 
 int mcgmil_conv2d_f32(const mcgmil_conv_args* a, void* stream) {
@@ -236,7 +303,9 @@ int mcgmil_conv2d_f32(const mcgmil_conv_args* a, void* stream) {
     const float* x = static_cast<const float*>(a->x);
     const float* w = static_cast<const float*>(a->w);
     float* y = static_cast<float*>(a->y);
-    return g.Cout % 128 == 0 ? launch32<2, 2>(g, x, w, y, s) : launch32<1, 4>(g, x, w, y, s);
+    if (g.Cin % kK != 0)
+        return g.Cout % 128 == 0 ? launch32<2, 2, true>(g, x, w, y, s) : launch32<1, 4, true>(g, x, w, y, s);
+    return g.Cout % 128 == 0 ? launch32<2, 2, false>(g, x, w, y, s) : launch32<1, 4, false>(g, x, w, y, s);
 }
 
 }  // extern "C"

@@ -30,7 +30,7 @@ EXPORTED = (
     "mcgmil_bn_args_size", "mcgmil_bn_workspace_size", "mcgmil_batchnorm_act",
     "mcgmil_batchnorm_coefficients", "mcgmil_conv_input_bn",
     "mcgmil_conv_args_size", "mcgmil_pack_conv_weights", "mcgmil_conv_stats_parts", "mcgmil_conv2d",
-    "mcgmil_pack_conv_weights_f32", "mcgmil_conv2d_f32",
+    "mcgmil_conv_packed_size_f32", "mcgmil_pack_conv_weights_f32", "mcgmil_conv2d_f32",
     "mcgmil_stem_args_size", "mcgmil_stem_packed_size", "mcgmil_pack_stem_weights",
     "mcgmil_stem_workspace_size", "mcgmil_stem_forward",
 )
@@ -199,6 +199,8 @@ def bind(path: str, mcdo_only: bool = False):
     L.mcgmil_conv_input_bn.restype = ctypes.c_int
     L.mcgmil_conv2d.argtypes = [pc, _vp]
     L.mcgmil_conv2d.restype = ctypes.c_int
+    L.mcgmil_conv_packed_size_f32.argtypes = [pc, ctypes.POINTER(ctypes.c_size_t)]
+    L.mcgmil_conv_packed_size_f32.restype = ctypes.c_int
     L.mcgmil_pack_conv_weights_f32.argtypes = [pc, _vp, _vp, _vp]
     L.mcgmil_pack_conv_weights_f32.restype = ctypes.c_int
     L.mcgmil_conv2d_f32.argtypes = [pc, _vp]

@@ -182,7 +182,8 @@ def conv32_enabled() -> bool:
 
 def conv32_fusable(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     """A CUDA channels-last fp32 activation (no autocast) and a convolution the fp32 kernel
-    implements (mcgmil_conv2d_f32: in_channels % 16, out_channels % 64, kernel <= 7), no autograd."""
+    implements (mcgmil_conv2d_f32: out_channels % 64, kernel <= 7, and in_channels % 16 or
+    kh * kw * in_channels <= 1024 -- the 3-channel stem), no autograd."""
     if not (conv32_enabled() and isinstance(conv, nn.Conv2d) and x.is_cuda and x.dim() == 4):
         return False
     if x.dtype != torch.float32 or torch.is_autocast_enabled("cuda"):
@@ -195,7 +196,9 @@ def conv32_fusable(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     kh, kw = conv.kernel_size
     if not (1 <= kh <= 7 and 1 <= kw <= 7):
         return False
-    if conv.in_channels % 16 or conv.out_channels % 64 or x.shape[1] != conv.in_channels:
+    if conv.out_channels % 64 or x.shape[1] != conv.in_channels:
+        return False
+    if conv.in_channels % 16 and kh * kw * conv.in_channels > 1024:
         return False
     if not x.is_contiguous(memory_format=torch.channels_last):
         return False
@@ -215,8 +218,10 @@ def packed_conv_weight_f32(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
         return cached[1]
     L = _lib.load()
     w32 = w.to(device=x.device, dtype=torch.float32).contiguous()
-    packed = torch.empty(w32.numel(), dtype=torch.float32, device=x.device)
     a = _conv_args(conv, x)
+    n = ctypes.c_size_t()
+    _lib.check(L.mcgmil_conv_packed_size_f32(ctypes.byref(a), ctypes.byref(n)), "mcgmil_conv_packed_size_f32")
+    packed = torch.empty(n.value, dtype=torch.float32, device=x.device)
     stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
     _lib.check(L.mcgmil_pack_conv_weights_f32(ctypes.byref(a), ctypes.c_void_p(w32.data_ptr()),
                                               ctypes.c_void_p(packed.data_ptr()), stream),
@@ -230,7 +235,7 @@ def conv2d_f32(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     activation (see conv32_fusable); returns a channels-last fp32 tensor."""
     if not conv32_fusable(conv, x):
         raise ValueError("conv2d_f32 needs a CUDA channels-last fp32 activation and a bias-free groups=1 "
-                         "convolution with in_channels % 16 == 0, out_channels % 64 == 0 (conv32_fusable)")
+                         "convolution with out_channels % 64 == 0 (conv32_fusable)")
     L = _lib.load()
     a = _conv_args(conv, x)
     oh = (a.height + 2 * a.pad - a.kernel_h) // a.stride + 1
@@ -525,7 +530,7 @@ def run_stem(conv: nn.Module, bn: nn.Module, pool: Optional[nn.Module], x: torch
         return stem(conv, bn, True, pool, x)
     if x.is_cuda and x.dim() == 4:
         x = x.contiguous(memory_format=torch.channels_last)
-    return bn_act(bn, torch_conv(conv, x), True, pool=pool)
+    return bn_act(bn, run_conv(conv, x), True, pool=pool)
 
 
 class DeferredBN(NamedTuple):

@@ -34,7 +34,7 @@ for s in ${STEPS:-fused all cfg5 bench}; do
         drift) step probe_drift 600 env PROBE_CPU=1 python -u scripts/probe_cfg5_drift.py bf16 fp32 fp32nochunk fp32torch ;;
         pmc) step pmc 1100 bash scripts/pmc_passes.sh ;;
         pmcab) step pmc_ab 1200 env PROBE_ROUNDS=1 PMC_CMD="python3 scripts/probe_fused.py" bash scripts/pmc_passes.sh ;;
-        conv32) step pytest_conv32 600 python -u -m pytest tests/test_gpu_conv32.py tests/test_gpu_features.py -m gpu -x -q -rf --timeout 300 --timeout-method thread ;;
+        conv32) step pytest_conv32 600 python -u -m pytest tests/test_gpu_conv32.py tests/test_gpu_features.py tests/test_gpu_pipeline.py -m gpu -x -q -rf --timeout 300 --timeout-method thread ;;
         probe32) step probe_conv32 600 python -u scripts/probe_conv32.py ;;
         cfg5f32) step bench_cfg5_fp32 900 python bench.py --workload cfg5 --features fp32 --steps 3 --warmup 1 --no-cpu-baseline ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

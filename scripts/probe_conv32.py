@@ -13,8 +13,8 @@ import torch.nn as nn
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "montecarlo-gated-mil_amd"))
 
-# (Cin, H, W, Cout, k, stride, pad) of ResNet-18's convolutions after the stem, per 224-px instance
-SHAPES = [(64, 56, 56, 64, 3, 1, 1), (64, 56, 56, 128, 3, 2, 1), (64, 56, 56, 128, 1, 2, 0),
+# (Cin, H, W, Cout, k, stride, pad) of ResNet-18's convolutions, per 224-px instance (the stem first)
+SHAPES = [(3, 224, 224, 64, 7, 2, 3), (64, 56, 56, 64, 3, 1, 1), (64, 56, 56, 128, 3, 2, 1), (64, 56, 56, 128, 1, 2, 0),
           (128, 28, 28, 128, 3, 1, 1), (128, 28, 28, 256, 3, 2, 1), (128, 28, 28, 256, 1, 2, 0),
           (256, 14, 14, 256, 3, 1, 1), (256, 14, 14, 512, 3, 2, 1), (256, 14, 14, 512, 1, 2, 0),
           (512, 7, 7, 512, 3, 1, 1)]

@@ -28,6 +28,11 @@ SHAPES = [
     (2, 16, 10, 10, 64, 5, 1, 2),
     (1, 48, 8, 13, 128, 7, 3, 3),
     (7, 32, 3, 5, 64, 1, 1, 0),
+    # gather mode (in_channels not a multiple of 16): the ResNet stem (7x7/2 from 3 channels, K =
+    # 147 padded to 160), an odd 5x5 from 5 channels, 1x1 from 24 channels
+    (3, 3, 64, 52, 64, 7, 2, 3),
+    (2, 5, 17, 9, 128, 5, 1, 2),
+    (4, 24, 6, 7, 64, 1, 1, 0),
 ]
 
 
@@ -84,6 +89,8 @@ def test_conv32_gates_and_repack(cuda):
             assert not conv32_fusable(conv, x)
         odd = _layer(64, 96, 3, 1, 1, cuda, 4)
         assert not conv32_fusable(odd, x)                                     # 96 % 64
+        x72 = torch.randn(2, 72, 12, 12, device=cuda).contiguous(memory_format=torch.channels_last)
+        assert not conv32_fusable(_layer(72, 64, 5, 1, 2, cuda, 5), x72)     # 5*5*72 > 1024, 72 % 16
         biased = nn.Conv2d(64, 64, 3, 1, 1, bias=True).to(cuda)
         assert not conv32_fusable(biased, x)
         os.environ["MCGMIL_NATIVE_CONV32"] = "0"
