@@ -369,6 +369,19 @@ __device__ __forceinline__ void score_rows(const GateParams& p, long long R0, fl
 // ---------------------------------------------------------------------------------------
 constexpr int kSoftmaxRows = 16;    // register path for bags of up to 4096 instances
 
+// A is written once and read by the host: MCGMIL_NT_A streams it past L2 (non-temporal), so the
+// ~1.6 MB of A a bag writes does not evict the H rows its other regions are about to re-read
+#ifndef MCGMIL_NT_A
+#define MCGMIL_NT_A 1
+#endif
+__device__ __forceinline__ void store_a(float* dst, float v) {
+#if MCGMIL_NT_A
+    __builtin_nontemporal_store(v, dst);
+#else
+    *dst = v;
+#endif
+}
+
 __device__ __forceinline__ void softmax_group(int ltid, bool active, int Nb, int C, const float* lg,
                                               const float* zz, float* Ao, float* Yo, float* sred) {
     const int tid = ltid, lane = ltid & 63, wave = ltid >> 6;
@@ -435,8 +448,8 @@ __device__ __forceinline__ void softmax_group(int ltid, bool active, int Nb, int
             for (int k = 0; k < kSoftmaxRows; ++k) {
                 const int n = tid + 256 * k;
                 if (n < Nl) {
-                    Ao[n] = e0[k] * inv0;
-                    Ao1[n] = e1[k] * inv1;
+                    store_a(Ao + n, e0[k] * inv0);
+                    store_a(Ao1 + n, e1[k] * inv1);
                 }
             }
         }
@@ -484,7 +497,7 @@ __device__ __forceinline__ void softmax_group(int ltid, bool active, int Nb, int
 #pragma unroll
                 for (int k = 0; k < kSoftmaxRows; ++k) {
                     const int n = tid + 256 * k;
-                    if (n < Nl) Aoc[n] = e[k] * inv;
+                    if (n < Nl) store_a(Aoc + n, e[k] * inv);
                 }
             }
             if (active && tid == 0) Yo[c] = y * inv;
@@ -514,7 +527,7 @@ __device__ __forceinline__ void softmax_group(int ltid, bool active, int Nb, int
         const float inv = 1.0f / s;
         if (Ao) {
             float* Aoc = Ao + (size_t)c * Nb;
-            for (int n = tid; n < Nl; n += 256) Aoc[n] = expf(lg[(size_t)n * C + c] - m) * inv;
+            for (int n = tid; n < Nl; n += 256) store_a(Aoc + n, expf(lg[(size_t)n * C + c] - m) * inv);
         }
         if (active && tid == 0) Yo[c] = y * inv;
     }
@@ -870,6 +883,11 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
 #ifndef MCGMIL_FUSED_NMAJOR
 #define MCGMIL_FUSED_NMAJOR 1
 #endif
+#ifndef MCGMIL_FUSED_REV
+#define MCGMIL_FUSED_REV 0         // 1: every other dispatch wave of an XCD sweeps its blocks backwards
+                                   // (H fetch 0.75x of forward alone, but 1.12x with MCGMIL_NT_A: off)
+#endif
+constexpr int kCUsPerXCD = 32;     // MI355X: 256 CUs in 8 XCDs, one fused workgroup per CU
 #ifndef MCGMIL_FUSED_CAP
 #define MCGMIL_FUSED_CAP 4096      // rows of one region's logits in LDS (C <= 2)
 #endif
@@ -906,6 +924,7 @@ __host__ __device__ inline int region_t_groups(int Nb, int T, int cap) {
 struct Region {
     int bag, t0, t1, Nb, ob;
     int ntiles, rot;               // 128-row tiles; the first one this workgroup runs
+    int rev;                       // instance blocks in descending order (MCGMIL_FUSED_REV)
     long long S, rows;
 };
 
@@ -917,7 +936,10 @@ struct Region {
 __device__ __forceinline__ int region_tile(const Region& rg, int i) {
 #if MCGMIL_FUSED_NMAJOR
     const int G = rg.t1 - rg.t0;
-    if (G > 1 && rg.Nb % kPipeBM == 0) return (i % G) * (rg.Nb / kPipeBM) + i / G;
+    if (G > 1 && rg.Nb % kPipeBM == 0) {
+        const int nb = rg.Nb / kPipeBM, blk = i / G;
+        return (i % G) * nb + (rg.rev ? nb - 1 - blk : blk);
+    }
 #endif
     const int k = i + rg.rot;
     return k < rg.ntiles ? k : k - rg.ntiles;
@@ -938,6 +960,7 @@ __device__ __forceinline__ GateParams reload_kernarg_params(const GateParams& p)
 
 __device__ __forceinline__ bool decode_region(const GateParams& p, int g, int cap, Region& rg) {
     int b, j, ts;
+    rg.rev = 0;
     if (p.uniform_rows > 0) {
         ts = p.region_t;
         const int rpb = (p.T + ts - 1) / ts;
@@ -948,6 +971,10 @@ __device__ __forceinline__ bool decode_region(const GateParams& p, int g, int ca
             const int k = g >> 3;
             b = 8 * (k / rpb) + (g & 7);
             j = k - (k / rpb) * rpb;
+            // the XCD's ~32 resident workgroups start and finish their regions together; a bag
+            // split over two such waves is re-read by the second, which then starts from the
+            // blocks the first read last (still in L2)
+            rg.rev = MCGMIL_FUSED_REV && ((k / kCUsPerXCD) & 1);
         } else {
             b = g / rpb;
             j = g - b * rpb;
