@@ -72,11 +72,7 @@ int launch(const mcgmil::GateParams& gp, long long total_rows, hipStream_t s) {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "plan_regions_kernel launch");
     }
-#ifdef MCGMIL_DIAG_TPW   // diagnostic: TPW flat tiles per workgroup (gate_fused_kernel)
-    const long long grid = (gp.total_samples / mcgmil::kPipeBM + MCGMIL_DIAG_TPW - 1) / MCGMIL_DIAG_TPW;
-#else
     const long long grid = fused_regions(gp, total_rows, cap, false);
-#endif
     if (grid == 0) return MCGMIL_OK;
     if (grid > 0x7fffffffll) return fail(MCGMIL_E_UNSUPPORTED, "too many regions for one launch");
     const size_t lds = mcgmil::fused_kernel_lds_bytes<E, MAXC>(gp.L);

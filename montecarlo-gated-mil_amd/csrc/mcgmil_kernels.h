@@ -65,9 +65,6 @@ struct GateParams {
 #define MCGMIL_STAMP(p, i) do {} while (0)
 #endif
 
-#ifndef MCGMIL_DIAG_H0
-#define MCGMIL_DIAG_H0 0   // diagnostic (timing only, wrong results): every bag reads bag 0's H rows
-#endif
 
 constexpr int kGateThreads = 512;  // 8 waves
 constexpr int kGateWaves = kGateThreads / kWave;
@@ -104,7 +101,7 @@ __device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0
             t = (int)(local / Nb);
             n = (int)(local - (long long)t * Nb);
         }
-        hrow = (MCGMIL_DIAG_H0 ? 0 : bag * Nb) + n;
+        hrow = bag * Nb + n;
     } else if (R < p.total_samples) {
         if (p.tile_bag) {
             bag = p.tile_bag[R0 / BM];
@@ -122,7 +119,7 @@ __device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0
             t = (int)(local / Nb);
             n = (int)(local - (long long)t * Nb);
         }
-        hrow = (MCGMIL_DIAG_H0 ? 0 : ob) + n;
+        hrow = ob + n;
     }
     int* ri = rinfo + kRowInfo * tid;
     ri[0] = hrow; ri[1] = t; ri[2] = n; ri[3] = bag; ri[4] = Nb;
@@ -860,20 +857,8 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
 // one t-group per region and go through the global workspace instead (the workgroup re-reads
 // its own writes).
 // ---------------------------------------------------------------------------------------
-#ifndef MCGMIL_FUSED_FLATROWS
-#define MCGMIL_FUSED_FLATROWS 0
-#endif
-#ifndef MCGMIL_FUSED_GLOBAL
-#define MCGMIL_FUSED_GLOBAL 0      // diagnostic: every region's scores through the global workspace
-#endif
 #ifndef MCGMIL_FUSED_XCD
 #define MCGMIL_FUSED_XCD 1         // 1: regions of bag b on XCD b % 8 (uniform bags, B % 8 == 0)
-#endif
-#ifndef MCGMIL_FUSED_ROT
-#define MCGMIL_FUSED_ROT 0         // 1: a region's tiles start at 5 j mod ntiles (region_tile)
-#endif
-#ifndef MCGMIL_FUSED_PIPE
-#define MCGMIL_FUSED_PIPE 0        // 1: fused_region_tiles (cross-tile pipeline), 0: pipe_tile per tile
 #endif
 #ifndef MCGMIL_FUSED_EARLY_HV
 #define MCGMIL_FUSED_EARLY_HV 0   // 1: head vectors before the K loop (as gate_pipe_kernel); in the
@@ -883,11 +868,6 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
 #ifndef MCGMIL_FUSED_NMAJOR
 #define MCGMIL_FUSED_NMAJOR 1
 #endif
-#ifndef MCGMIL_FUSED_REV
-#define MCGMIL_FUSED_REV 0         // 1: every other dispatch wave of an XCD sweeps its blocks backwards
-                                   // (H fetch 0.75x of forward alone, but 1.12x with MCGMIL_NT_A: off)
-#endif
-constexpr int kCUsPerXCD = 32;     // MI355X: 256 CUs in 8 XCDs, one fused workgroup per CU
 #ifndef MCGMIL_FUSED_CAP
 #define MCGMIL_FUSED_CAP 4096      // rows of one region's logits in LDS (C <= 2)
 #endif
@@ -923,26 +903,21 @@ __host__ __device__ inline int region_t_groups(int Nb, int T, int cap) {
 
 struct Region {
     int bag, t0, t1, Nb, ob;
-    int ntiles, rot;               // 128-row tiles; the first one this workgroup runs
-    int rev;                       // instance blocks in descending order (MCGMIL_FUSED_REV)
+    int ntiles;                    // 128-row tiles
     long long S, rows;
 };
 
 // Tile i of a region's run order. MCGMIL_FUSED_NMAJOR: when the region is G > 1 t-groups of
 // whole tiles, instance-block major -- tile i reads the same 128 H rows as tile i-1 for G-1 of
-// every G tiles, so each block comes from beyond L2 once per region instead of G times.
-// MCGMIL_FUSED_ROT: the bag's j-th region starts at tile 5 j (mod ntiles). The order changes no
-// result: every tile's logits land at their own rows, and the softmax runs after the last tile.
+// every G tiles, so each block comes from beyond L2 once per region instead of G times. The order
+// changes no result: every tile's logits land at their own rows, and the softmax runs after the
+// last tile.
 __device__ __forceinline__ int region_tile(const Region& rg, int i) {
 #if MCGMIL_FUSED_NMAJOR
     const int G = rg.t1 - rg.t0;
-    if (G > 1 && rg.Nb % kPipeBM == 0) {
-        const int nb = rg.Nb / kPipeBM, blk = i / G;
-        return (i % G) * nb + (rg.rev ? nb - 1 - blk : blk);
-    }
+    if (G > 1 && rg.Nb % kPipeBM == 0) return (i % G) * (rg.Nb / kPipeBM) + i / G;
 #endif
-    const int k = i + rg.rot;
-    return k < rg.ntiles ? k : k - rg.ntiles;
+    return i;
 }
 
 // The kernel's parameters (its only argument, at offset 0 of the kernarg segment) read again
@@ -960,7 +935,6 @@ __device__ __forceinline__ GateParams reload_kernarg_params(const GateParams& p)
 
 __device__ __forceinline__ bool decode_region(const GateParams& p, int g, int cap, Region& rg) {
     int b, j, ts;
-    rg.rev = 0;
     if (p.uniform_rows > 0) {
         ts = p.region_t;
         const int rpb = (p.T + ts - 1) / ts;
@@ -971,10 +945,6 @@ __device__ __forceinline__ bool decode_region(const GateParams& p, int g, int ca
             const int k = g >> 3;
             b = 8 * (k / rpb) + (g & 7);
             j = k - (k / rpb) * rpb;
-            // the XCD's ~32 resident workgroups start and finish their regions together; a bag
-            // split over two such waves is re-read by the second, which then starts from the
-            // blocks the first read last (still in L2)
-            rg.rev = MCGMIL_FUSED_REV && ((k / kCUsPerXCD) & 1);
         } else {
             b = g / rpb;
             j = g - b * rpb;
@@ -994,7 +964,6 @@ __device__ __forceinline__ bool decode_region(const GateParams& p, int g, int ca
     rg.S = (long long)p.T * rg.ob + (long long)rg.t0 * rg.Nb;
     rg.rows = (long long)(rg.t1 - rg.t0) * rg.Nb;
     rg.ntiles = (int)((rg.rows + kPipeBM - 1) / kPipeBM);
-    rg.rot = MCGMIL_FUSED_ROT && rg.ntiles > 0 ? (int)(((long long)j * 5) % rg.ntiles) : 0;
     return true;
 }
 
@@ -1011,189 +980,13 @@ __device__ __forceinline__ void fill_row_table_region(const GateParams& p, const
         const uint32_t tt = r / (uint32_t)rg.Nb;
         n = (int)(r - tt * (uint32_t)rg.Nb);
         t = rg.t0 + (int)tt;
-        hrow = (MCGMIL_DIAG_H0 ? 0 : rg.ob) + n;
+        hrow = rg.ob + n;
     }
     int* ri = rinfo + kRowInfo * tid;
     ri[0] = hrow; ri[1] = t; ri[2] = n; ri[3] = rg.bag; ri[4] = rg.Nb;
     ri[5] = (int)(p.bag_ids ? p.bag_ids[rg.bag] : p.bag_base + (uint32_t)rg.bag);
 }
 
-
-// ---------------------------------------------------------------------------------------
-// fused_region_tiles -- the region's tiles as ONE software pipeline (MCGMIL_FUSED_PIPE=1).
-// The K loop of pipe_tile prefetches H two steps and the weights one step ahead; in a region the
-// next tile's rows are known, so the prefetches of the last K steps fetch the NEXT tile's first H
-// chunks and step-0 weights, and the last step stages the next tile's step 0 (Philox included)
-// into the idle slot. The next tile's K loop then starts right after this tile's epilogue: no row
-// table, no prologue loads, no prologue barrier per tile. Row info is arithmetic (a region is
-// t-groups of one bag). The MFMA sequence, the masks and the epilogue are pipe_tile's, so the
-// logits are bitwise the same.
-// ---------------------------------------------------------------------------------------
-template <typename E>
-struct RowState {          // a thread's staging row (= its scoring row) in one tile
-    const E* hsrc;         // H row + its 8-element chunk kq (row 0 for padding rows)
-    uint32_t n, t;         // instance, sample (t_base included)
-    uint32_t inval;        // 0, or ~0 for a padding row (stages zeros, no score)
-};
-
-template <typename E>
-__device__ __forceinline__ RowState<E> region_row(const GateParams& p, const Region& rg, int tile,
-                                                 int srow, int kq) {
-    RowState<E> s;
-    const long long rho = (long long)tile * kPipeBM + srow;
-    const E* H = reinterpret_cast<const E*>(p.H);
-    if (rho < rg.rows) {
-        const uint32_t r = (uint32_t)rho;
-        const uint32_t tt = r / (uint32_t)rg.Nb;
-        s.n = r - tt * (uint32_t)rg.Nb;
-        s.t = (uint32_t)(p.t_base + rg.t0) + tt;
-        s.hsrc = H + (size_t)((MCGMIL_DIAG_H0 ? 0 : rg.ob) + (int)s.n) * p.ldh + kq * 8;
-        s.inval = 0u;
-    } else {
-        s.n = 0u;
-        s.t = 0u;
-        s.hsrc = H + kq * 8;
-        s.inval = 0xFFFFFFFFu;
-    }
-    return s;
-}
-
-template <typename E, int PPW, int MAXC, bool ONE_CLASS>
-__device__ __forceinline__ void fused_region_tiles(const GateParams& p0, Region* srg, int ntiles,
-                                                   E* Xs, float* red, float* zred, float* slg,
-                                                   float* szz, E* zw) {
-    constexpr int BM = kPipeBM;
-    constexpr int RT = BM / 16;
-    constexpr int NJ = 2 * PPW;
-    constexpr int SLOT = RT * 64 * 8;
-    constexpr int CAP = fused_cap<MAXC>();
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int kq = lane >> 4;
-    const int srow = wave * 16 + (lane & 15);
-
-    // the region's first tile: prologue loads and the staging of its step 0
-    Region rg0 = *srg;
-    const uint32_t cb = p0.bag_ids ? (uint32_t)p0.bag_ids[rg0.bag] : p0.bag_base + (uint32_t)rg0.bag;
-    RowState<E> cur = region_row<E>(p0, rg0, region_tile(rg0, 0), srow, kq);
-    const __amdgpu_buffer_rsrc_t wrs0 = make_rsrc(p0.Wp, p0.wp_bytes);
-    const int KS0 = p0.L >> 5;
-    const uint32_t tile_bytes0 = (uint32_t)KS0 * 512u * (uint32_t)sizeof(E);
-    const uint32_t lane_b = (uint32_t)lane * 8u * (uint32_t)sizeof(E);
-    const int q00 = __builtin_amdgcn_readfirstlane(wave) * PPW;
-    Frag<E> wA[NJ], wB[NJ], zA, zB;
-    Raw<E> hA, hB;
-    hA = load_raw(cur.hsrc);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        int q = q00 + (j >> 1);
-        q = q < p0.P ? q : p0.P - 1;
-        wA[j] = load_frag_buf<E>(wrs0, lane_b, (uint32_t)(2 * q + (j & 1)) * tile_bytes0);
-    }
-    if constexpr (fused_zl<E>())   // the classifier fragments of all K steps, once per workgroup
-        load_classifier_lds<E>(wrs0, (uint32_t)(2 * p0.P) * tile_bytes0, KS0, zw);
-    else
-        zA = load_frag_buf<E>(wrs0, lane_b, (uint32_t)(2 * p0.P) * tile_bytes0);
-    hB = load_raw(cur.hsrc + 32);
-    {
-        const uint4 o = philox4x32_10<true>((uint32_t)kq, cur.n, cur.t, cb, p0.k0, p0.k1);
-        store_dropped(hA, o, p0.thrx_f, cur.inval, Xs + tid * 8);
-    }
-    __syncthreads();
-
-    for (int i = 0; i < ntiles; ++i) {
-        const GateParams p = reload_kernarg_params(p0);
-        Region* qr = srg;
-        asm volatile("" : "+v"(qr));
-        const Region rg = *qr;
-        const int KS = p.L >> 5;
-        const long long R0 = rg.S + (long long)region_tile(rg, i) * BM;
-
-        const __amdgpu_buffer_rsrc_t wrs = make_rsrc(p.Wp, p.wp_bytes);
-        const uint32_t tile_bytes = (uint32_t)KS * 512u * (uint32_t)sizeof(E);
-        constexpr uint32_t kStepBytes = 512u * (uint32_t)sizeof(E);
-        const int q0 = __builtin_amdgcn_readfirstlane(wave) * PPW;
-        uint32_t wsoff[NJ];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            int q = q0 + (j >> 1);
-            q = q < p.P ? q : p.P - 1;
-            wsoff[j] = (uint32_t)(2 * q + (j & 1)) * tile_bytes;
-        }
-        const uint32_t zsoff = (uint32_t)(2 * p.P) * tile_bytes;
-        auto wfrag = [&](uint32_t soff) { return load_frag_buf<E>(wrs, lane_b, soff); };
-
-        f32x4 acc[RT][NJ];
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        f32x4 zacc = {0.f, 0.f, 0.f, 0.f};
-
-        // K step s: MFMAs from slot `cur_slot`; weights of step s+1 (mod KS: the next tile's step 0
-        // at the last step), H of step s+2 and the staging of step s+1 from row state `hs` / `ss`
-        // (this tile's, or the next tile's once the step index wraps).
-        auto kstep = [&](int s, const E* cs, E* ns, const Frag<E> (&w)[NJ], const Frag<E>& z,
-                         Frag<E> (&wn)[NJ], Frag<E>& zn, const Raw<E>& h, Raw<E>& hn,
-                         const RowState<E>& hs, int hstep, const RowState<E>& ss, int sstep) {
-            const int s1 = s + 1 < KS ? s + 1 : 0;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) wn[j] = wfrag(wsoff[j] + (uint32_t)s1 * kStepBytes);
-            if constexpr (!fused_zl<E>()) zn = wfrag(zsoff + (uint32_t)s1 * kStepBytes);
-            hn = load_raw(hs.hsrc + (size_t)hstep * 32);
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt) {
-                const Frag<E> x = load_frag(cs + (size_t)(rt * 64 + lane) * 8);
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) acc[rt][j] = mma(w[j], x, acc[rt][j]);
-            }
-            const Frag<E> xz = load_frag(cs + (size_t)tid * 8);
-            if constexpr (fused_zl<E>()) zacc = mma(load_frag(zw + (size_t)(s * 64 + lane) * 8), xz, zacc);
-            else zacc = mma(z, xz, zacc);
-            {
-                const uint4 o = philox4x32_10<true>((uint32_t)(sstep * 4 + kq), ss.n, ss.t, cb, p.k0, p.k1);
-                store_dropped(h, o, p.thrx_f, ss.inval, ns + tid * 8);
-            }
-            if constexpr (sizeof(E) == 2 && PPW == 2) {
-#pragma unroll
-                for (int k = 0; k < RT * NJ + 1; ++k) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0); // VALU
-                }
-            }
-            __syncthreads();
-        };
-
-        constexpr bool kEarlyHV = MCGMIL_FUSED_EARLY_HV && ONE_CLASS && sizeof(E) == 2;
-        HeadVec hvec[PPW];
-        if constexpr (kEarlyHV) load_head_vectors<PPW>(p, q0, lane, hvec);
-        // steps 0, 1 peeled (zero accumulators as inline constants), 2 .. KS-3 in pairs, and the
-        // last two peeled: their H prefetches and the last staging belong to the next tile
-        kstep(0, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA, cur, 2, cur, 1);
-        kstep(1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB, cur, 3, cur, 2);
-        for (int s = 2; s < KS - 2; s += 2) {
-            kstep(s, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA, cur, s + 2, cur, s + 1);
-            kstep(s + 1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB, cur, s + 3, cur, s + 2);
-        }
-        // the next tile's rows (this tile's again after the last one: loads in range, unused),
-        // computed here so that they are not live through the K loop
-        const RowState<E> nxt = region_row<E>(p, rg, region_tile(rg, i + 1 < ntiles ? i + 1 : i), srow, kq);
-        kstep(KS - 2, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA, nxt, 0, cur, KS - 1);
-        kstep(KS - 1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB, nxt, 1, nxt, 0);
-
-        float part[MAXC][RT];
-#pragma unroll
-        for (int c = 0; c < MAXC; ++c)
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt) part[c][rt] = 0.f;
-        fold_pairs<RT, PPW, MAXC, ONE_CLASS>(p, acc, q0, lane, part, kEarlyHV ? hvec : nullptr);
-        const int one_class = ONE_CLASS ? (q0 < p.P ? q0 / (p.D >> 4) : MAXC) : -1;
-        const bool lds = rg.Nb <= CAP && !MCGMIL_FUSED_GLOBAL;
-        score_rows<BM, MAXC>(p, R0, part, zacc, red, zred, one_class,
-                             ONE_CLASS ? (p.D >> 4) / PPW : 0, cur.inval == 0u, cur.t, cur.n, cb,
-                             lds ? slg : p.logits, lds ? szz : p.zz, lds ? rg.S : 0);
-        cur = nxt;
-    }
-}
 
 template <typename E, int PPW, int MAXC, bool ONE_CLASS>
 __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GateParams p) {
@@ -1208,19 +1001,6 @@ __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GatePara
     float* szz = slg + CAP * MAXC;                                        // [CAP][C]
     float* sred = szz + CAP * MAXC;                                       // [2][16]
 
-#ifdef MCGMIL_DIAG_TPW   // diagnostic (timing only, no A/Y): TPW consecutive flat tiles per workgroup
-    for (int i = 0; i < MCGMIL_DIAG_TPW; ++i) {
-        const GateParams pt = reload_kernarg_params(p);
-        const long long R0 = ((long long)blockIdx.x * MCGMIL_DIAG_TPW + i) * BM;
-        if (R0 >= pt.total_samples) break;
-        int* ri = rinfo + (i & 1) * kRowInfo * BM;
-        fill_row_table<BM>(pt, R0, ri);
-        __syncthreads();
-        pipe_tile<E, PPW, MAXC, false, ONE_CLASS, MCGMIL_FUSED_EARLY_HV>(pt, R0, Xs, red, zred, ri,
-                                                                         pt.logits, pt.zz, 0);
-    }
-    return;
-#endif
 #if MCGMIL_DIAG & 64   // diagnostic (timing only): gate_pipe_kernel's work in this kernel's frame
     {
         const long long R0 = (long long)blockIdx.x * BM;
@@ -1240,12 +1020,6 @@ __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GatePara
     // 256 VGPRs.
     Region* srg = reinterpret_cast<Region*>(sred + 32);
     if (threadIdx.x == 0) *srg = rg;                 // read after the first tile's barrier
-#if MCGMIL_FUSED_PIPE
-    __syncthreads();                                 // the region in LDS
-    if (ntiles > 0)
-        fused_region_tiles<E, PPW, MAXC, ONE_CLASS>(p, srg, ntiles, Xs, red, zred, slg, szz,
-                                                    reinterpret_cast<E*>(smem + fused_lds_bytes<E, MAXC>()));
-#else
     E* zw = reinterpret_cast<E*>(smem + fused_lds_bytes<E, MAXC>());
     if constexpr (fused_zl<E>())
         load_classifier_lds<E>(make_rsrc(p.Wp, p.wp_bytes), (uint32_t)(2 * p.P) * (uint32_t)(p.L >> 5) * 512u *
@@ -1259,27 +1033,22 @@ __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GatePara
         MCGMIL_STAMP(pt, 0);
         {
             const Region r = *qr;
-#if MCGMIL_FUSED_FLATROWS   // diagnostic: the flat kernel's row table (uniform bags, whole tiles)
-            fill_row_table<BM>(pt, r.S + (long long)region_tile(r, i) * BM, ri);
-#else
             fill_row_table_region<BM>(pt, r, r.S + (long long)region_tile(r, i) * BM, ri);
-#endif
         }
         __syncthreads();
         MCGMIL_STAMP(pt, 1);
         const Region r = *qr;
-        const bool lds = r.Nb <= CAP && !MCGMIL_FUSED_GLOBAL;
+        const bool lds = r.Nb <= CAP;
         pipe_tile<E, PPW, MAXC, false, ONE_CLASS, MCGMIL_FUSED_EARLY_HV, fused_zl<E>(), false>(
             pt, r.S + (long long)region_tile(r, i) * BM, Xs, red, zred, ri, lds ? slg : pt.logits,
             lds ? szz : pt.zz, lds ? r.S : 0, zw);
     }
-#endif
     __syncthreads();
 #if MCGMIL_DIAG & 32   // ablation (timing only, no A/Y): no softmax phase
     if (ntiles >= 0) return;
 #endif
     rg = *srg;
-    const bool in_lds = rg.Nb <= CAP && !MCGMIL_FUSED_GLOBAL;
+    const bool in_lds = rg.Nb <= CAP;
 
     // softmax + pooling per t-group (model.py:305-316), two groups at a time
     const int G = rg.t1 - rg.t0;

@@ -28,8 +28,7 @@ for s in ${STEPS:-fused all cfg5 bench}; do
         abfused) step ab_fused 300 env MCGMIL_PROBE_LIBS="$(ls -1 abvar/*.so abvar2/*.so 2>/dev/null | paste -sd, -)" python -u scripts/probe_fused.py ;;
         abfused128) step ab_fused128 300 env PROBE_N=128 MCGMIL_PROBE_LIBS="$(ls -1 abvar/*.so abvar2/*.so 2>/dev/null | paste -sd, -)" python -u scripts/probe_fused.py ;;
         stamps) step stamps_flat 300 env PROBE_BAGS=128 python -u scripts/probe_stamps.py
-                step stamps_fused 300 env PROBE_BAGS=128 PROBE_FUSED=1 STAMP_DEFINES=MCGMIL_FUSED_PIPE=0 python -u scripts/probe_stamps.py
-                step stamps_fused_flatrows 300 env PROBE_BAGS=128 PROBE_FUSED=1 STAMP_DEFINES=MCGMIL_FUSED_PIPE=0,MCGMIL_FUSED_FLATROWS=1 python -u scripts/probe_stamps.py ;;
+                step stamps_fused 300 env PROBE_BAGS=128 PROBE_FUSED=1 python -u scripts/probe_stamps.py ;;
         listpmc) step list_pmc 120 rocprofv3 --list-avail ;;
         drift) step probe_drift 600 env PROBE_CPU=1 python -u scripts/probe_cfg5_drift.py bf16 fp32 fp32nochunk fp32torch ;;
         pmc) step pmc 1100 bash scripts/pmc_passes.sh ;;

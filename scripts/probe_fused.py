@@ -2,7 +2,8 @@
 (gate_pipe_kernel + softmax_pool_kernel), interleaved in one process, optionally over several
 variant builds of the library (MCGMIL_PROBE_LIBS=a.so,b.so; scripts/build_variants.sh).
 
-Config 3 shape (N=2048, T=100, bf16, separate heads), PROBE_BAGS bags per launch (default 128).
+Config 3 shape (N=2048, T=100, bf16, separate heads; PROBE_N, PROBE_T and PROBE_DTYPE=f32 change
+it), PROBE_BAGS bags per launch (default 128).
 Per (library, path): median ms of the gate(+softmax) launch(es) by HIP events, algorithmic
 TFLOP/s, and whether Y and A are bitwise equal to the first library's two-kernel path."""
 import ctypes
@@ -25,16 +26,17 @@ def main():
     paths = [p for p in os.environ.get("MCGMIL_PROBE_LIBS", "").split(",") if p]
     libs = {os.path.basename(p): _lib.bind(p, mcdo_only=True) for p in paths} or {"libmcgmil.so": base}
     dev = torch.device("cuda", 0)
-    N, T, L, D, C = int(os.environ.get("PROBE_N", "2048")), 100, 512, 128, 2
+    N, T, L, D, C = int(os.environ.get("PROBE_N", "2048")), int(os.environ.get("PROBE_T", "100")), 512, 128, 2
+    dt = torch.float32 if os.environ.get("PROBE_DTYPE", "bf16") == "f32" else torch.bfloat16
     B = int(os.environ.get("PROBE_BAGS", str(128 * 2048 // N)))
     rounds = int(os.environ.get("PROBE_ROUNDS", "5"))
     g = torch.Generator(device=dev).manual_seed(0)
-    H = torch.randn(B * N, L, device=dev, generator=g).abs_().bfloat16()
+    H = torch.randn(B * N, L, device=dev, generator=g).abs_().to(dt)
     offs = ops.bag_offsets_tensor([N] * B, dev)
     sd = synthetic.head_state_dict(0, L=L, D=D, C=C, shared=False)
     arrays = synthetic.head_arrays(sd, C, False)
     head = ops.HeadTensors(*[torch.from_numpy(arrays[k]).to(dev) for k in ops.HeadTensors._fields])
-    packed = ops.packed_weights(head, torch.bfloat16)
+    packed = ops.packed_weights(head, dt)
     a = ops.make_args(H, offs, head, T, C, C, D, 0.1, 0.1, seed=42)
     a.packed_w = ctypes.c_void_p(packed.data_ptr())
     Y = torch.empty(B, T, C, device=dev)
