@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct mcgmil_bn_args {
     int64_t rows;               /* N * H * W */
-    int32_t channels;           /* C, multiple of 8, <= 4096 */
+    int32_t channels;           /* C, multiple of 8, <= 2048 */
     int32_t dtype;              /* MCGMIL_BF16 or MCGMIL_F32 (x, residual and y) */
     const void* x;              /* [rows, C] */
     const void* residual;       /* [rows, C] added before the activation, or NULL */
@@ -72,8 +72,11 @@ typedef struct mcgmil_bn_args {
     void* workspace;            /* >= mcgmil_bn_workspace_size() bytes, 256-byte aligned */
     size_t workspace_bytes;
     const float* partials;      /* optional [num_partials][3][C] (count, mean, M2) blocks of x, as
-                                   mcgmil_conv2d's stats: batch statistics from them (Chan's
-                                   combination in fp64, fixed order) instead of a pass over x */
+                                   mcgmil_conv2d's / mcgmil_conv2d_f32's stats: batch statistics
+                                   from them (Chan's combination in fp64, fixed order) instead of
+                                   a pass over x. More than 1024 blocks are first combined in
+                                   chunks of consecutive blocks (fp64, stored as fp32 blocks) in
+                                   the workspace, so size it after setting partials */
     const float* residual_ab;   /* optional [2][C] (a_c, b_c) of the residual's own BatchNorm (as
                                    mcgmil_batchnorm_coefficients writes them): the added residual
                                    is dtype(fmaf(r, a_c, b_c)) -- bit-identical to normalising the
@@ -165,9 +168,14 @@ int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream);
  * packed fp32 weight made by mcgmil_pack_conv_weights_f32 from the torch layout [out, in, kh, kw]
  * fp32 (mcgmil_conv_packed_size_f32 floats). out_channels a multiple of 64, kernel 1..7, and
  * in_channels a multiple of 16 or kernel_h * kernel_w * in_channels <= 1024 (the 3-channel stem,
- * one 4-byte gather per element); no in_ab, no stats (MCGMIL_E_UNSUPPORTED). 16-byte aligned
- * pointers. */
+ * one 4-byte gather per element). 16-byte aligned pointers.
+ *   stats: as mcgmil_conv2d's, one (count, mean, M2) block per output-pixel tile of the fp32
+ *     outputs, parts = mcgmil_conv_stats_parts_f32().
+ *   in_ab / in_relu: as mcgmil_conv2d's, in fp32 (max(fmaf(x, a_c, b_c), 0) or fmaf(x, a_c, b_c),
+ *     bit-identical to mcgmil_batchnorm_act then mcgmil_conv2d_f32); in_channels a multiple of 16
+ *     and <= 2048 (not the gather mode), else MCGMIL_E_UNSUPPORTED. */
 int mcgmil_conv_packed_size_f32(const mcgmil_conv_args* a, size_t* floats);
+int mcgmil_conv_stats_parts_f32(const mcgmil_conv_args* a, int32_t* parts);
 int mcgmil_pack_conv_weights_f32(const mcgmil_conv_args* a, const void* weight, void* packed, void* stream);
 int mcgmil_conv2d_f32(const mcgmil_conv_args* a, void* stream);
 int mcgmil_bn_workspace_size(const mcgmil_bn_args* a, size_t* bytes);
@@ -175,7 +183,8 @@ int mcgmil_batchnorm_act(const mcgmil_bn_args* a, void* stream);
 /* The per-channel coefficients mcgmil_batchnorm_act would apply, without the apply pass:
  * ab[c] = a_c = gamma_c / sqrt(var_c + eps), ab[C + c] = b_c = beta_c - mean_c * a_c (fp32,
  * [2][C], 4-byte aligned). Statistics as mcgmil_batchnorm_act: from partials, from the running
- * statistics, or from a pass over x (then workspace as mcgmil_bn_workspace_size). y, residual and
+ * statistics, or from a pass over x (then, and with more than 1024 partials, workspace as
+ * mcgmil_bn_workspace_size). y, residual and
  * the pooling fields are ignored; batch_mean / batch_invstd are written when given. For a consumer
  * that applies the BatchNorm itself (mcgmil_conv_args.in_ab). */
 int mcgmil_batchnorm_coefficients(const mcgmil_bn_args* a, float* ab, void* stream);

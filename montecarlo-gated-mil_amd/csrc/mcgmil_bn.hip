@@ -33,6 +33,8 @@ constexpr int kMaxParts = 1024;       // statistics workgroups
 constexpr long long kBytesPerPart = 64 << 10;   // at least this much input per statistics workgroup
 constexpr int kFinCh = 8;             // finalize: channels per workgroup
 constexpr int kFinLanes = kThreads / kFinCh;    // finalize: lanes per channel
+constexpr int kMaxChanParts = 1024;   // (count, mean, M2) blocks the finalize combines directly
+constexpr int kChanChunks = 512;      // above that: chunks of consecutive blocks, at most this many
 
 __device__ __forceinline__ void load8(const __bf16* p, float (&v)[8]) {
     const uint4 u = *reinterpret_cast<const uint4*>(p);
@@ -241,6 +243,30 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_chan_kernel(const float*
     write_ab(c, C, mean, var, gamma, beta, eps, ab, bmean, binvstd);
 }
 
+// More than kMaxChanParts blocks (an fp32 convolution's one block per pixel tile): chunk j of
+// `chunk` consecutive blocks -> one block out[j], thread per channel (coalesced across channels),
+// the finalize's fp64 combination around the chunk's first mean, stored back as (n, mean, M2).
+__global__ __launch_bounds__(kThreads) void bn_chan_reduce_kernel(const float* __restrict__ part, int parts,
+                                                                int C, int chunk, float* __restrict__ out) {
+    const int c = blockIdx.y * kThreads + threadIdx.x;
+    if (c >= C) return;
+    const int b0 = blockIdx.x * chunk, b1 = b0 + chunk < parts ? b0 + chunk : parts;
+    const double m0 = (double)part[((size_t)b0 * 3 + 1) * C + c];
+    double n = 0.0, S = 0.0, Q = 0.0;
+#pragma unroll 4
+    for (int b = b0; b < b1; ++b) {
+        const double nb = (double)part[((size_t)b * 3) * C + c];
+        const double d = (double)part[((size_t)b * 3 + 1) * C + c] - m0;
+        n += nb;
+        S = fma(nb, d, S);
+        Q += fma(nb * d, d, (double)part[((size_t)b * 3 + 2) * C + c]);
+    }
+    const double M2 = n > 0.0 ? Q - S * S / n : 0.0;
+    out[((size_t)blockIdx.x * 3) * C + c] = (float)n;
+    out[((size_t)blockIdx.x * 3 + 1) * C + c] = (float)(n > 0.0 ? m0 + S / n : 0.0);
+    out[((size_t)blockIdx.x * 3 + 2) * C + c] = (float)(M2 > 0.0 ? M2 : 0.0);
+}
+
 // Grid-stride over 8-channel vectors; the total thread count is a multiple of C/8, so every
 // thread keeps one channel group. Two vectors in flight per iteration.
 // RESBN: the residual gets its own BatchNorm first, rounded to E as a separate pass would store it
@@ -402,9 +428,21 @@ int parts_for(const mcgmil_bn_args* a) {
     return (int)(p < kMaxParts ? (p < 1 ? 1 : p) : kMaxParts);
 }
 
+// blocks per chunk when the producer's partials are reduced first (0: combined directly)
+int chan_chunk(const mcgmil_bn_args* a) {
+    if (!a->partials || a->running_mean || a->num_partials <= kMaxChanParts) return 0;
+    return (a->num_partials + kChanChunks - 1) / kChanChunks;
+}
+
+// [2][C] a, b, then the statistics pass's [parts][2][C] sums or the reduced [chunks][3][C] blocks
 size_t ws_bytes(const mcgmil_bn_args* a) {
-    const size_t f = (size_t)2 * a->channels * (1 + (size_t)parts_for(a));
-    return (f * sizeof(float) + 255) & ~(size_t)255;
+    const size_t C = (size_t)a->channels;
+    size_t tail = 2 * C * (size_t)parts_for(a);
+    if (const int ch = chan_chunk(a)) {
+        const size_t red = 3 * C * (size_t)((a->num_partials + ch - 1) / ch);
+        tail = red > tail ? red : tail;
+    }
+    return ((2 * C + tail) * sizeof(float) + 255) & ~(size_t)255;
 }
 
 int validate(const mcgmil_bn_args* a) {
@@ -529,8 +567,18 @@ int run(const mcgmil_bn_args* a, hipStream_t s, float* ab_out = nullptr) {
     const E* x = static_cast<const E*>(a->x);
     if (!a->running_mean && a->partials) {       // statistics from the producer's (n, mean, M2)
         float* ab = ab_out ? ab_out : static_cast<float*>(a->workspace);
+        const float* blocks = a->partials;
+        int nblocks = a->num_partials;
+        if (const int ch = chan_chunk(a)) {
+            float* red = static_cast<float*>(a->workspace) + 2 * C;
+            const int chunks = (nblocks + ch - 1) / ch;
+            hipLaunchKernelGGL(bn_chan_reduce_kernel, dim3((unsigned)chunks, (unsigned)((C + kThreads - 1) / kThreads)),
+                               dim3(kThreads), 0, s, blocks, nblocks, C, ch, red);
+            blocks = red;
+            nblocks = chunks;
+        }
         hipLaunchKernelGGL(bn_finalize_chan_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kThreads), 0, s,
-                           a->partials, a->num_partials, C, a->gamma, a->beta, a->eps, ab, a->batch_mean,
+                           blocks, nblocks, C, a->gamma, a->beta, a->eps, ab, a->batch_mean,
                            a->batch_invstd);
         if (ab_out) {
             const hipError_t e = hipGetLastError();
@@ -605,7 +653,8 @@ int mcgmil_batchnorm_coefficients(const mcgmil_bn_args* a, float* ab, void* stre
     if (int rc = validate(&b)) return rc;
     const bool pass = !b.running_mean && !b.partials;     // statistics from a pass over x
     if (pass && !a->x) return fail(MCGMIL_E_INVALID, "batch statistics without partials need x");
-    if (pass && (!b.workspace || b.workspace_bytes < ws_bytes(&b) || ((uintptr_t)b.workspace & 255)))
+    if ((pass || chan_chunk(&b)) &&
+        (!b.workspace || b.workspace_bytes < ws_bytes(&b) || ((uintptr_t)b.workspace & 255)))
         return fail(MCGMIL_E_WORKSPACE, "workspace missing, misaligned or smaller than "
                                         "mcgmil_bn_workspace_size()");
     hipStream_t s = static_cast<hipStream_t>(stream);

@@ -207,21 +207,6 @@ struct LaneStats {
     }
 };
 
-// (n, m, M2) <- merge with (nb, mb, M2b) for every channel (the counts are shared by the channels)
-template <int NCH>
-__device__ __forceinline__ void chan_merge(float& n, float (&m)[NCH], float (&M2)[NCH], float nb,
-                                           const float (&mb)[NCH], const float (&M2b)[NCH]) {
-    const float nn = n + nb;
-    const float f = nn > 0.f ? nb / nn : 0.f, h = n * f;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const float d = mb[c] - m[c];
-        m[c] = fmaf(d, f, m[c]);
-        M2[c] = M2[c] + M2b[c] + d * d * h;
-    }
-    n = nn;
-}
-
 // End of kernel: lanes -> (n, mean, M2); merged over the 16 pixel lanes of each channel group
 // (butterfly, the lane-0 result kept), then over the WGM waves that share channels (LDS, wave
 // order). Lane channel of index c = 4 i + v: chan0 + 16 i + 4 (lane >> 4) + v (local to the

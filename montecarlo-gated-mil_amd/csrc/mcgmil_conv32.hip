@@ -15,11 +15,20 @@
 // one k read 16 consecutive words and the 16-word row pad puts the next k on the next 16 banks:
 // every ds_read_b32 is conflict-free. The C layout gives a lane 4 consecutive output channels of
 // one pixel: one 16-byte store per tile.
+//
+// INBN: the input BatchNorm of the previous layer (mcgmil_conv_args.in_ab) is applied to the B
+// elements as they are written to LDS (after the step's MFMAs, so the loads stay in flight), so
+// relu(bn(x)) is never materialised. STATS: the epilogue also reduces its outputs to one
+// (count, mean, M2) block per channel of the tile (shifted sums over a wave's pixels, then the
+// waves sharing the channels; tile_stats) for the BatchNorm that follows, so the activation is
+// not re-read for statistics.
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 #include "../../include/mcgmil.h"
 #include "../../include/mcgmil_features.h"
+#include "mcgmil_device.h"
 #include "mcgmil_error.h"
 
 namespace {
@@ -34,12 +43,16 @@ struct Conv32Geom {
     long long P;          // N * OH * OW output pixels
     int KS;               // K steps of 16: KH * KW * Cin / 16, or ceil(KH * KW * Cin / 16) (gather)
     int Ktot;             // KH * KW * Cin
+    const float* in_ab;   // INBN: [2][Cin] a_c then b_c
+    float in_lo;          // INBN: floor after the BatchNorm, 0 (ReLU) or -inf
+    float* stats;         // STATS: [pixel tiles][3][Cout] (count, mean, M2)
 };
 
 // Gather mode (in_channels not a multiple of 16: the 3-channel stem): K is the flattened
 // (kh, kw, ci) of the NHWC window, zero-padded to whole steps, and every B element is its own
 // 4-byte load through a per-workgroup LDS table of k -> (offset in the window, kh, kw).
 constexpr int kMaxGatherK = 1024;
+constexpr int kMaxInBnC = 2048;     // INBN: a_c, b_c of up to this many input channels in LDS
 
 constexpr int kK = 16;    // K step (input channels of one tap)
 constexpr int kPad = 16;  // LDS row pad (words)
@@ -52,13 +65,89 @@ struct Tile {
     static constexpr int A4 = kK * BN_CO / 4 / 256, B4 = kK * BM_PX / 4 / 256;   // float4 per thread
 };
 
-template <int WCO, int WPX, bool GATHER>
-__global__ __launch_bounds__(256) void conv32_kernel(const Conv32Geom g, const float* __restrict__ x,
+// Lane 15 of every row of 16 lanes gets the row's sum (DPP row_shr 1, 2, 4, 8: four VALU adds,
+// no LDS traffic); the other lanes hold partial sums.
+__device__ __forceinline__ float row_sum16(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xF, 0xF, true));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xF, 0xF, true));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xF, 0xF, true));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xF, 0xF, true));
+    return v;
+}
+
+// The tile's statistics (STATS): see the header comment. acc[i][j]: channels 16 i + 4 kl + v of
+// the wave's 64, pixels 16 j + cl; the wave's first nval pixels are valid. Per channel the 16
+// lanes sum x - sh and (x - sh)^2 around sh = the channel's output at the wave's first pixel
+// (lane 16 kl, j = 0), row_sum16 adds the lanes, and lane 16 kl + 15 turns the sums into the
+// wave's (count, mean, M2); the waves sharing the channels are merged by chan_merge. One channel quad i
+// at a time, so few registers are live beside the accumulators, and no division per lane.
+template <int WCO, int WPX>
+__device__ __forceinline__ void tile_stats(const f32x4 (&acc)[4][4], int nval, int wco, int wpx, int lane,
+                                           float* red, float* stats, long long row, int Cout, int co0) {
+    using T = Tile<WCO, WPX>;
+    const int kl = lane >> 4, cl = lane & 15;
+    const float n = (float)nval, rn = nval > 0 ? 1.f / n : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float sh[4], S[4], Q[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            sh[v] = __shfl(acc[i][0][v], kl * 16, 64);
+            float sum = 0.f, sq = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float d = 16 * j + cl < nval ? acc[i][j][v] - sh[v] : 0.f;
+                sum += d;
+                sq = fmaf(d, d, sq);
+            }
+            S[v] = sum;
+            Q[v] = sq;
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            S[v] = row_sum16(S[v]);
+            Q[v] = row_sum16(Q[v]);
+        }
+        if (cl == 15) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int local = wco * 64 + 16 * i + 4 * kl + v;
+                red[(wpx * 3 + 0) * T::BN_CO + local] = n;
+                red[(wpx * 3 + 1) * T::BN_CO + local] = nval > 0 ? fmaf(S[v], rn, sh[v]) : 0.f;
+                red[(wpx * 3 + 2) * T::BN_CO + local] = nval > 0 ? fmaxf(Q[v] - S[v] * S[v] * rn, 0.f) : 0.f;
+            }
+        }
+    }
+    __syncthreads();
+    for (int local = threadIdx.x; local < T::BN_CO; local += 256) {
+        float cn = red[local], cm[1] = {red[T::BN_CO + local]}, cM2[1] = {red[2 * T::BN_CO + local]};
+        for (int w = 1; w < WPX; ++w) {
+            const float mb[1] = {red[(w * 3 + 1) * T::BN_CO + local]}, M2b[1] = {red[(w * 3 + 2) * T::BN_CO + local]};
+            mcgmil::chan_merge<1>(cn, cm, cM2, red[(w * 3) * T::BN_CO + local], mb, M2b);
+        }
+        stats[((size_t)row * 3 + 0) * Cout + co0 + local] = cn;
+        stats[((size_t)row * 3 + 1) * Cout + co0 + local] = cm[0];
+        stats[((size_t)row * 3 + 2) * Cout + co0 + local] = cM2[0];
+    }
+}
+
+// STATS: 4 waves per SIMD (<= 128 registers with the 64 accumulators): the 128 x 128 tile's LDS
+// allows 4 workgroups per CU, and without the bound the statistics epilogue's peak (148 registers)
+// cost one of them. The other variants fit 128 unbounded (accumulators in AGPRs).
+template <int WCO, int WPX, bool GATHER, bool INBN, bool STATS>
+__global__ __launch_bounds__(256, STATS ? 4 : 1) void conv32_kernel(const Conv32Geom g, const float* __restrict__ x,
                                                      const float* __restrict__ w, float* __restrict__ y) {
     using T = Tile<WCO, WPX>;
+    static_assert(!(GATHER && INBN), "the gather mode has no input BatchNorm");
     extern __shared__ __attribute__((aligned(16))) float smem32[];
     // gather table after the two stages: k -> window offset (floats) and kh | kw << 8
     int* gtab = reinterpret_cast<int*>(smem32 + 2 * T::STAGE);
+    // INBN: the input BatchNorm's a_c, b_c after the two stages
+    float* sab = smem32 + 2 * T::STAGE;
+    if constexpr (INBN) {
+        for (int c = threadIdx.x; c < 2 * g.Cin; c += 256) sab[c] = g.in_ab[c];
+        __syncthreads();
+    }
     if constexpr (GATHER) {
         const int kpad = g.KS * kK;
         for (int k = threadIdx.x; k < kpad; k += 256) {
@@ -98,6 +187,8 @@ __global__ __launch_bounds__(256) void conv32_kernel(const Conv32Geom g, const f
     const int cchunks = g.Cin / kK > 0 ? g.Cin / kK : 1;
 
     f32x4 ra[T::A4], rb[T::B4];
+    bool bin = false;     // INBN: the staged B quads are in-image x (BatchNorm them; padding stays 0)
+    int bci0 = 0;         // INBN: their first input channel
     auto load = [&](int ks) {
         // A: packed weights [KS][16][Cout], rows k of this K step, columns co0 .. co0 + BN_CO
         const float* wk = w + (long long)ks * kK * g.Cout + co0;
@@ -130,6 +221,10 @@ __global__ __launch_bounds__(256) void conv32_kernel(const Conv32Geom g, const f
         const int kh = tap / g.KW, kw = tap - kh * g.KW;
         const int ih = ih0 + kh, iw = iw0 + kw;
         const bool in = pvalid && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        if constexpr (INBN) {
+            bin = in;
+            bci0 = ci0;
+        }
         const float* src = xn + ((long long)(in ? ih : 0) * g.W + (in ? iw : 0)) * g.Cin + ci0;
 #pragma unroll
         for (int r = 0; r < T::B4; ++r) {
@@ -149,6 +244,16 @@ __global__ __launch_bounds__(256) void conv32_kernel(const Conv32Geom g, const f
 #pragma unroll
         for (int r = 0; r < T::B4; ++r) {
             const int q = bq0 + QSTEP * r;
+            if constexpr (INBN) {   // bitwise mcgmil_batchnorm_act's max(fmaf(x, a, b), lo)
+                if (bin) {
+                    const f32x4 a = *reinterpret_cast<const f32x4*>(sab + bci0 + 4 * q);
+                    const f32x4 b = *reinterpret_cast<const f32x4*>(sab + g.Cin + bci0 + 4 * q);
+                    rb[r].x = fmaxf(fmaf(rb[r].x, a.x, b.x), g.in_lo);
+                    rb[r].y = fmaxf(fmaf(rb[r].y, a.y, b.y), g.in_lo);
+                    rb[r].z = fmaxf(fmaf(rb[r].z, a.z, b.z), g.in_lo);
+                    rb[r].w = fmaxf(fmaf(rb[r].w, a.w, b.w), g.in_lo);
+                }
+            }
             Bs[(4 * q + 0) * T::BS + bpx] = rb[r].x;
             Bs[(4 * q + 1) * T::BS + bpx] = rb[r].y;
             Bs[(4 * q + 2) * T::BS + bpx] = rb[r].z;
@@ -199,6 +304,11 @@ __global__ __launch_bounds__(256) void conv32_kernel(const Conv32Geom g, const f
 #pragma unroll
         for (int i = 0; i < 4; ++i) *reinterpret_cast<f32x4*>(yp + 16 * i) = acc[i][j];
     }
+    if constexpr (STATS) {   // the stages are free: the K loop ended with a barrier
+        const long long left = g.P - (px0 + wpx * 64);
+        tile_stats<WCO, WPX>(acc, left < 0 ? 0 : (left > 64 ? 64 : (int)left), wco, wpx, lane, smem32,
+                             g.stats, blockIdx.x, g.Cout, co0);
+    }
 }
 
 // torch layout [Cout, Cin, KH, KW] fp32 -> [KS][16][Cout]: row r = ks * 16 + k of K = (kh, kw, ci)
@@ -241,7 +351,9 @@ int validate32(const mcgmil_conv_args* a, Conv32Geom* g) {
     if (a->kernel_h < 1 || a->kernel_w < 1 || a->kernel_h > 7 || a->kernel_w > 7)
         return fail(MCGMIL_E_UNSUPPORTED, "kernel size must be in 1..7");
     if (a->stride < 1 || a->pad < 0 || a->pad > 64) return fail(MCGMIL_E_INVALID, "stride >= 1 and 0 <= pad <= 64");
-    if (a->in_ab || a->stats) return fail(MCGMIL_E_UNSUPPORTED, "fp32 convolution: no in_ab / stats");
+    if (a->in_ab && (a->in_channels % kK != 0 || a->in_channels > kMaxInBnC))
+        return fail(MCGMIL_E_UNSUPPORTED, "fp32 convolution: in_ab needs in_channels a multiple of 16, <= 2048");
+    if (a->in_relu != 0 && a->in_relu != 1) return fail(MCGMIL_E_INVALID, "in_relu must be 0 or 1");
     const long long oh = ((long long)a->height + 2 * a->pad - a->kernel_h) / a->stride + 1;
     const long long ow = ((long long)a->width + 2 * a->pad - a->kernel_w) / a->stride + 1;
     if (oh < 1 || ow < 1) return fail(MCGMIL_E_INVALID, "the kernel does not fit the padded input");
@@ -253,18 +365,41 @@ int validate32(const mcgmil_conv_args* a, Conv32Geom* g) {
         g->stride = a->stride; g->pad = a->pad; g->OH = (int)oh; g->OW = (int)ow; g->P = P;
         g->Ktot = a->kernel_h * a->kernel_w * a->in_channels;
         g->KS = (g->Ktot + kK - 1) / kK;
+        g->in_ab = a->in_ab;
+        g->in_lo = a->in_relu ? 0.f : -INFINITY;
+        g->stats = a->stats;
     }
     return MCGMIL_OK;
 }
 
-template <int WCO, int WPX, bool GATHER>
+template <int WCO, int WPX>
+long long pixel_tiles(const Conv32Geom& g) { return (g.P + Tile<WCO, WPX>::BM_PX - 1) / Tile<WCO, WPX>::BM_PX; }
+
+// 128 x 128 tiles when Cout is a multiple of 128, else 64 x 256
+bool wide_co(const Conv32Geom& g) { return g.Cout % 128 == 0; }
+
+template <int WCO, int WPX, bool GATHER, bool INBN, bool STATS>
 int launch32(const Conv32Geom& g, const float* x, const float* w, float* y, hipStream_t s) {
     using T = Tile<WCO, WPX>;
-    const size_t lds = (size_t)2 * T::STAGE * sizeof(float) + (GATHER ? (size_t)g.KS * kK * 8 : 0);
-    dim3 grid((unsigned)((g.P + T::BM_PX - 1) / T::BM_PX), (unsigned)(g.Cout / T::BN_CO));
-    hipLaunchKernelGGL((conv32_kernel<WCO, WPX, GATHER>), grid, dim3(256), lds, s, g, x, w, y);
+    const size_t lds = (size_t)2 * T::STAGE * sizeof(float) + (GATHER ? (size_t)g.KS * kK * 8 : 0) +
+                       (INBN ? (size_t)2 * g.Cin * sizeof(float) : 0);
+    dim3 grid((unsigned)pixel_tiles<WCO, WPX>(g), (unsigned)(g.Cout / T::BN_CO));
+    hipLaunchKernelGGL((conv32_kernel<WCO, WPX, GATHER, INBN, STATS>), grid, dim3(256), lds, s, g, x, w, y);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "conv32_kernel launch");
+}
+
+template <int WCO, int WPX>
+int dispatch32(const Conv32Geom& g, const float* x, const float* w, float* y, hipStream_t s) {
+    const bool st = g.stats != nullptr;
+    if (g.Cin % kK != 0)
+        return st ? launch32<WCO, WPX, true, false, true>(g, x, w, y, s)
+                  : launch32<WCO, WPX, true, false, false>(g, x, w, y, s);
+    if (g.in_ab)
+        return st ? launch32<WCO, WPX, false, true, true>(g, x, w, y, s)
+                  : launch32<WCO, WPX, false, true, false>(g, x, w, y, s);
+    return st ? launch32<WCO, WPX, false, false, true>(g, x, w, y, s)
+              : launch32<WCO, WPX, false, false, false>(g, x, w, y, s);
 }
 
 }  // namespace
@@ -293,19 +428,29 @@ int mcgmil_conv_packed_size_f32(const mcgmil_conv_args* a, size_t* floats) {
     return MCGMIL_OK;
 }
 
+int mcgmil_conv_stats_parts_f32(const mcgmil_conv_args* a, int32_t* parts) {
+    Conv32Geom g;
+    if (int rc = validate32(a, &g)) return rc;
+    if (!parts) return fail(MCGMIL_E_INVALID, "parts is NULL");
+    const long long t = wide_co(g) ? pixel_tiles<2, 2>(g) : pixel_tiles<1, 4>(g);
+    if (t > 0x7fffffffll) return fail(MCGMIL_E_UNSUPPORTED, "too many pixel tiles");
+    *parts = (int32_t)t;
+    return MCGMIL_OK;
+}
+
 int mcgmil_conv2d_f32(const mcgmil_conv_args* a, void* stream) {
     Conv32Geom g;
     if (int rc = validate32(a, &g)) return rc;
     if (!a->x || !a->w || !a->y) return fail(MCGMIL_E_INVALID, "NULL x, w or y");
     if (((uintptr_t)a->x | (uintptr_t)a->w | (uintptr_t)a->y) & 15u)
         return fail(MCGMIL_E_ALIGN, "x, w and y must be 16-byte aligned");
+    if (((uintptr_t)a->stats | (uintptr_t)a->in_ab) & 3u)
+        return fail(MCGMIL_E_ALIGN, "stats and in_ab must be 4-byte aligned");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const float* x = static_cast<const float*>(a->x);
     const float* w = static_cast<const float*>(a->w);
     float* y = static_cast<float*>(a->y);
-    if (g.Cin % kK != 0)
-        return g.Cout % 128 == 0 ? launch32<2, 2, true>(g, x, w, y, s) : launch32<1, 4, true>(g, x, w, y, s);
-    return g.Cout % 128 == 0 ? launch32<2, 2, false>(g, x, w, y, s) : launch32<1, 4, false>(g, x, w, y, s);
+    return wide_co(g) ? dispatch32<2, 2>(g, x, w, y, s) : dispatch32<1, 4>(g, x, w, y, s);
 }
 
 }  // extern "C"

@@ -212,4 +212,21 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
+// BatchNorm statistics blocks (count, mean, M2): (n, m, M2) <- merge with (nb, mb, M2b) for every
+// channel, Chan's pairwise update (the counts are shared by the channels). The convolution
+// epilogues (mcgmil_conv.hip, mcgmil_conv32.hip) reduce their outputs' statistics with it.
+template <int NCH>
+__device__ __forceinline__ void chan_merge(float& n, float (&m)[NCH], float (&M2)[NCH], float nb,
+                                           const float (&mb)[NCH], const float (&M2b)[NCH]) {
+    const float nn = n + nb;
+    const float f = nn > 0.f ? nb / nn : 0.f, h = n * f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const float d = mb[c] - m[c];
+        m[c] = fmaf(d, f, m[c]);
+        M2[c] = M2[c] + M2b[c] + d * d * h;
+    }
+    n = nn;
+}
+
 }  // namespace mcgmil

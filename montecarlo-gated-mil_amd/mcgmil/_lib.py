@@ -31,6 +31,7 @@ EXPORTED = (
     "mcgmil_batchnorm_coefficients", "mcgmil_conv_input_bn",
     "mcgmil_conv_args_size", "mcgmil_pack_conv_weights", "mcgmil_conv_stats_parts", "mcgmil_conv2d",
     "mcgmil_conv_packed_size_f32", "mcgmil_pack_conv_weights_f32", "mcgmil_conv2d_f32",
+    "mcgmil_conv_stats_parts_f32",
     "mcgmil_stem_args_size", "mcgmil_stem_packed_size", "mcgmil_pack_stem_weights",
     "mcgmil_stem_workspace_size", "mcgmil_stem_forward",
 )
@@ -201,6 +202,8 @@ def bind(path: str, mcdo_only: bool = False):
     L.mcgmil_conv2d.restype = ctypes.c_int
     L.mcgmil_conv_packed_size_f32.argtypes = [pc, ctypes.POINTER(ctypes.c_size_t)]
     L.mcgmil_conv_packed_size_f32.restype = ctypes.c_int
+    L.mcgmil_conv_stats_parts_f32.argtypes = [pc, ctypes.POINTER(ctypes.c_int32)]
+    L.mcgmil_conv_stats_parts_f32.restype = ctypes.c_int
     L.mcgmil_pack_conv_weights_f32.argtypes = [pc, _vp, _vp, _vp]
     L.mcgmil_pack_conv_weights_f32.restype = ctypes.c_int
     L.mcgmil_conv2d_f32.argtypes = [pc, _vp]

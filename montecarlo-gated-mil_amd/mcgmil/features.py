@@ -230,23 +230,60 @@ def packed_conv_weight_f32(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     return packed
 
 
-def conv2d_f32(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+def conv32_input_bn(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """Whether conv2d_f32(conv, x, in_ab=...) can apply an input BatchNorm (in_channels a multiple
+    of 16, <= 2048: every fp32 kernel but the gather mode); False with MCGMIL_FUSE_INPUT_BN=0."""
+    return fold_enabled() and conv32_fusable(conv, x) and conv.in_channels % 16 == 0 and \
+        conv.in_channels <= 2048
+
+
+def conv2d_f32(conv: nn.Conv2d, x: torch.Tensor, stats: bool = False,
+               in_ab: Optional[torch.Tensor] = None, in_relu: bool = True):
     """conv(x) in fp32 on the MFMA kernel (fp32 operands and accumulation) for a channels-last fp32
-    activation (see conv32_fusable); returns a channels-last fp32 tensor."""
+    activation (see conv32_fusable); returns a channels-last fp32 tensor, or with stats=True
+    (y, partials): the BatchNorm statistics of y as [pixel tiles, 3, Cout] (count, mean, M2)
+    blocks for batchnorm_act(..., partials=...). With in_ab ([2, Cin] fp32 from
+    batchnorm_coefficients) the convolution reads relu?(bn(x)) instead of x (conv32_input_bn)."""
     if not conv32_fusable(conv, x):
         raise ValueError("conv2d_f32 needs a CUDA channels-last fp32 activation and a bias-free groups=1 "
                          "convolution with out_channels % 64 == 0 (conv32_fusable)")
     L = _lib.load()
     a = _conv_args(conv, x)
+    if in_ab is not None:
+        if in_ab.shape != (2, a.in_channels) or in_ab.dtype != torch.float32 or \
+                in_ab.device != x.device or not in_ab.is_contiguous():
+            raise ValueError("in_ab must be a contiguous fp32 [2, in_channels] tensor on x's device")
+        a.in_ab, a.in_relu = ctypes.c_void_p(in_ab.data_ptr()), int(bool(in_relu))
     oh = (a.height + 2 * a.pad - a.kernel_h) // a.stride + 1
     ow = (a.width + 2 * a.pad - a.kernel_w) // a.stride + 1
     y = torch.empty((a.batch, a.out_channels, oh, ow), dtype=torch.float32, device=x.device,
                     memory_format=torch.channels_last)
     w = packed_conv_weight_f32(conv, x)
     a.x, a.w, a.y = (ctypes.c_void_p(t.data_ptr()) for t in (x, w, y))
+    part = None
+    if stats:
+        n = ctypes.c_int32()
+        _lib.check(L.mcgmil_conv_stats_parts_f32(ctypes.byref(a), ctypes.byref(n)), "mcgmil_conv_stats_parts_f32")
+        part = torch.empty((n.value, 3, a.out_channels), dtype=torch.float32, device=x.device)
+        a.stats = ctypes.c_void_p(part.data_ptr())
     stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
     _lib.check(L.mcgmil_conv2d_f32(ctypes.byref(a), stream), "mcgmil_conv2d_f32")
-    return y
+    return (y, part) if stats else y
+
+
+def _native_conv(conv: nn.Module, x: torch.Tensor) -> Optional[str]:
+    """"bf16" (conv2d), "f32" (conv2d_f32) or None (the torch layer) for conv on x."""
+    if isinstance(conv, nn.Conv2d):
+        if conv_fusable(conv, x):
+            return "bf16"
+        if conv32_fusable(conv, x):
+            return "f32"
+    return None
+
+
+def _takes_input_bn(conv: nn.Module, x: torch.Tensor) -> bool:
+    kind = _native_conv(conv, x)
+    return (kind == "bf16" and conv_input_bn(conv, x)) or (kind == "f32" and conv32_input_bn(conv, x))
 
 
 def torch_conv(layer: nn.Module, x: torch.Tensor) -> torch.Tensor:
@@ -388,7 +425,7 @@ def batchnorm_coefficients(x: torch.Tensor, bn: nn.BatchNorm2d,
                 partials.dtype != torch.float32 or partials.device != dev:
             raise ValueError("partials must be a contiguous fp32 [parts, 3, C] tensor on x's device")
         a.partials, a.num_partials = p(partials), partials.shape[0]
-    elif use_batch:
+    if use_batch:     # the statistics pass, or more than 1024 partials combined in chunks first
         n = ctypes.c_size_t()
         a.y = a.x
         _lib.check(L.mcgmil_bn_workspace_size(ctypes.byref(a), ctypes.byref(n)), "mcgmil_bn_workspace_size")
@@ -530,6 +567,12 @@ def run_stem(conv: nn.Module, bn: nn.Module, pool: Optional[nn.Module], x: torch
         return stem(conv, bn, True, pool, x)
     if x.is_cuda and x.dim() == 4:
         x = x.contiguous(memory_format=torch.channels_last)
+    if isinstance(conv, nn.Conv2d) and conv32_fusable(conv, x) and isinstance(bn, nn.BatchNorm2d) \
+            and _use_batch(bn):
+        y, part = conv2d_f32(conv, x, stats=True)    # statistics from the convolution's epilogue
+        if fusable(y, bn) and (pool is None or _pool_params(pool) is not None):
+            return batchnorm_act(y, bn, True, pool=pool, partials=part)
+        return bn_act(bn, y, True, pool=pool)
     return bn_act(bn, run_conv(conv, x), True, pool=pool)
 
 
@@ -552,9 +595,10 @@ def _use_batch(bn: nn.BatchNorm2d) -> bool:
 
 def conv_bn_act(conv: nn.Module, bn: nn.Module, x, relu: bool, residual=None,
                 consumer: Optional[nn.Module] = None, as_residual: bool = False):
-    """The blocks' `relu?(bn(conv(x)) [+ residual])`: on the GPU the MFMA convolution also emits
-    the BatchNorm batch statistics of its output (when the BN normalises with them), and the fused
-    BN consumes them -- the activation is written once and read once. Else run_conv + bn_act.
+    """The blocks' `relu?(bn(conv(x)) [+ residual])`: on the GPU the MFMA convolution (bf16 or
+    fp32) also emits the BatchNorm batch statistics of its output (when the BN normalises with
+    them), and the fused BN consumes them -- the activation is written once and read once. Else
+    run_conv + bn_act.
     x may be a DeferredBN (its BN runs inside this convolution). With `consumer` (the convolution
     that reads the result) and no residual, the result may come back as a DeferredBN when that
     convolution can apply the BN itself (conv_input_bn); pass it on to conv_bn_act. With
@@ -568,20 +612,22 @@ def conv_bn_act(conv: nn.Module, bn: nn.Module, x, relu: bool, residual=None,
             res_deferred, residual, res_ab = residual, residual.y, residual.ab
     kw = {}
     if isinstance(x, DeferredBN):
-        if isinstance(conv, nn.Conv2d) and conv_fusable(conv, x.y) and conv_input_bn(conv, x.y):
+        if _takes_input_bn(conv, x.y):
             kw = {"in_ab": x.ab, "in_relu": x.relu}
             x = x.y
         else:
             x = x.materialise()
-    if isinstance(conv, nn.Conv2d) and conv_fusable(conv, x):
+    kind = _native_conv(conv, x)
+    if kind is not None:
+        native = conv2d if kind == "bf16" else conv2d_f32
         if isinstance(bn, nn.BatchNorm2d) and _use_batch(bn):
-            y, part = conv2d(conv, x, stats=True, **kw)
+            y, part = native(conv, x, stats=True, **kw)
         else:
-            y, part = conv2d(conv, x, **kw), None
+            y, part = native(conv, x, **kw), None
         if not (isinstance(bn, nn.BatchNorm2d) and fusable(y, bn, residual)):
             return bn_act(bn, y, relu, res_deferred.materialise() if res_deferred else residual)
-        if residual is None and ((isinstance(consumer, nn.Conv2d) and conv_fusable(consumer, y)
-                                  and conv_input_bn(consumer, y)) or (as_residual and not relu and fold_enabled())):
+        if residual is None and ((isinstance(consumer, nn.Conv2d) and _takes_input_bn(consumer, y))
+                                 or (as_residual and not relu and fold_enabled())):
             return DeferredBN(y, batchnorm_coefficients(y, bn, part), relu, bn, part)
         return batchnorm_act(y, bn, relu, residual, partials=part, residual_ab=res_ab)
     return bn_act(bn, run_conv(conv, x), relu, res_deferred.materialise() if res_deferred else residual)

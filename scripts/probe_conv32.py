@@ -1,7 +1,8 @@
 """Time the fp32 backbone convolution (mcgmil_conv2d_f32) against MIOpen's fp32 convolution (the
 torch layer, channels-last) on ResNet-18's convolution shapes at a config-5 bag (k instances,
-default 1,507), interleaved in one process. Prints one JSON line per shape: ms and TFLOP/s of each,
-and the max |diff| / max |ref| between them."""
+default 1,507), interleaved in one process; also the native one with its BatchNorm statistics
+epilogue (stats) and with an input BatchNorm too (stats_inbn). Prints one JSON line per shape:
+ms and TFLOP/s of each, and the max |diff| / max |ref| between native and MIOpen."""
 import json
 import os
 import statistics
@@ -31,14 +32,20 @@ def main():
         x = torch.randn(N, cin, h, w, device=dev).contiguous(memory_format=torch.channels_last)
         oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
         flops = 2.0 * N * oh * ow * cout * cin * k * k
-        times = {"native": [], "miopen": []}
+        times = {"native": [], "miopen": [], "stats": [], "stats_inbn": []}
+        ab = torch.stack([torch.rand(cin, device=dev) + 0.5, torch.randn(cin, device=dev)]).contiguous()
+        fns = {"native": lambda: conv2d_f32(conv, x), "miopen": lambda: torch_conv(conv, x),
+               "stats": lambda: conv2d_f32(conv, x, stats=True),
+               "stats_inbn": lambda: conv2d_f32(conv, x, stats=True, in_ab=ab)}
+        if cin % 16:
+            del fns["stats_inbn"], times["stats_inbn"]
         with torch.no_grad():
             a = conv2d_f32(conv, x)
             b = torch_conv(conv, x)
             torch.cuda.synchronize()
             diff = float((a - b).abs().max() / b.abs().max())
             for _ in range(rounds):
-                for name, fn in (("native", lambda: conv2d_f32(conv, x)), ("miopen", lambda: torch_conv(conv, x))):
+                for name, fn in fns.items():
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                     fn()

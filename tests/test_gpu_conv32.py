@@ -105,3 +105,116 @@ def test_conv32_gates_and_repack(cuda):
         y2 = conv2d_f32(conv, x)
         assert torch.allclose(y2, 2 * y, rtol=1e-6, atol=1e-6)
     assert not conv32_fusable(conv, x)                                        # grad enabled, weight needs grad
+
+
+def _combine(part):
+    """fp64 Chan combination of [parts, 3, C] (count, mean, M2) blocks -> (count, mean, var)."""
+    p = part.double()
+    n, m, M2 = p[:, 0], p[:, 1], p[:, 2]
+    N = n.sum(0)
+    mean = (n * m).sum(0) / N
+    var = (M2 + n * (m - mean) ** 2).sum(0) / N
+    return N, mean, var
+
+
+# (N, Cin, H, W, Cout, k, stride, pad): both tile shapes (Cout 64: 64 x 256, else 128 x 128), a
+# last pixel tile that is partly empty, the gather-mode stem, a 1x1 stride-2 downsample
+STATS_SHAPES = [
+    (3, 64, 20, 20, 64, 3, 1, 1),
+    (2, 64, 17, 13, 128, 3, 2, 1),
+    (2, 3, 40, 36, 64, 7, 2, 3),
+    (3, 128, 9, 9, 256, 1, 2, 0),
+]
+
+
+@pytest.mark.parametrize("shape", STATS_SHAPES)
+def test_conv2d_f32_stats(cuda, shape):
+    """The epilogue's (count, mean, M2) blocks combine to the fp64 mean / variance of the fp32
+    outputs themselves, over every output pixel; y is unchanged by computing them."""
+    from mcgmil.features import conv2d_f32
+    N, Cin, H, W, Cout, k, s, p = shape
+    conv = _layer(Cin, Cout, k, s, p, cuda, 11 + Cin)
+    x = torch.randn(N, Cin, H, W, device=cuda, generator=torch.Generator(device=cuda).manual_seed(H))
+    x = x.contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        y, part = conv2d_f32(conv, x, stats=True)
+        torch.cuda.synchronize()
+        assert torch.equal(y, conv2d_f32(conv, x))
+    cnt, mean, var = _combine(part)
+    yd = y.double().permute(0, 2, 3, 1).reshape(-1, Cout)
+    assert bool((cnt == yd.shape[0]).all())
+    rmean, rvar = yd.mean(0), yd.var(0, unbiased=False)
+    scale = rvar.sqrt() + rmean.abs()
+    assert float(((mean - rmean).abs() / scale).max()) <= 1e-6
+    assert float(((var - rvar).abs() / rvar).max()) <= 1e-5
+
+
+@pytest.mark.parametrize("relu", [True, False])
+@pytest.mark.parametrize("shape", [(3, 64, 15, 11, 64, 3, 1, 1), (2, 128, 9, 9, 256, 3, 2, 1),
+                                   (2, 64, 12, 12, 128, 1, 2, 0)])
+def test_conv2d_f32_input_bn_bitwise(cuda, shape, relu):
+    """conv(relu?(bn(x))) with the BatchNorm applied while staging (in_ab) is bit-identical to
+    mcgmil_batchnorm_act followed by the plain convolution -- padding stays zero."""
+    from mcgmil.features import batchnorm_act, batchnorm_coefficients, conv2d_f32, conv32_input_bn
+    N, Cin, H, W, Cout, k, s, p = shape
+    conv = _layer(Cin, Cout, k, s, p, cuda, 5 + Cout)
+    g = torch.Generator(device=cuda).manual_seed(N + W)
+    x = (torch.randn(N, Cin, H, W, device=cuda, generator=g) * 3 + 1).contiguous(memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(Cin).to(cuda)
+    with torch.no_grad():
+        bn.weight.copy_(torch.randn(Cin, device=cuda, generator=g))
+        bn.bias.copy_(torch.randn(Cin, device=cuda, generator=g))
+    bn.eval()
+    bn.running_mean, bn.running_var = None, None          # batch statistics, as the reference
+    bn.track_running_stats = False
+    with torch.no_grad():
+        assert conv32_input_bn(conv, x)
+        ab = batchnorm_coefficients(x, bn)
+        y_in = conv2d_f32(conv, x, in_ab=ab, in_relu=relu)
+        y_ref = conv2d_f32(conv, batchnorm_act(x, bn, relu))
+        torch.cuda.synchronize()
+    assert torch.equal(y_in, y_ref)
+
+
+def test_bn_many_partials(cuda):
+    """More than 1024 statistics blocks (an fp32 layer-1 convolution's one block per 256-pixel
+    tile) are combined in chunks first: the result matches a statistics pass over y, through
+    both mcgmil_batchnorm_act and mcgmil_batchnorm_coefficients."""
+    from mcgmil.features import batchnorm_act, batchnorm_coefficients, conv2d_f32
+    conv = _layer(64, 64, 3, 1, 1, cuda, 21)
+    x = torch.randn(90, 64, 56, 56, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3))
+    x = x.contiguous(memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(64, track_running_stats=False).to(cuda).eval()
+    with torch.no_grad():
+        y, part = conv2d_f32(conv, x, stats=True)
+        assert part.shape[0] > 1024
+        a1 = batchnorm_act(y, bn, True, partials=part)
+        a2 = batchnorm_act(y, bn, True)
+        c1 = batchnorm_coefficients(y, bn, part)
+        c2 = batchnorm_coefficients(y, bn)
+        torch.cuda.synchronize()
+    assert float((a1 - a2).abs().max()) <= 1e-5 * float(a2.abs().max())
+    assert float(((c1 - c2).abs() / c2.abs().clamp_min(1e-3)).max()) <= 1e-5
+
+
+def test_backbone_f32_input_bn_bitwise(cuda):
+    """The fp32 backbone with the BatchNorms folded into the next convolution (and the downsample
+    BN into the residual add) is bit-identical to the one that materialises every BN output."""
+    from mcgmil.resnet import build_backbone, deactivate_batchnorm, Identity
+    import os
+    outs = []
+    for fold in ("1", "0"):
+        os.environ["MCGMIL_FUSE_INPUT_BN"] = fold
+        try:
+            torch.manual_seed(0)
+            net = build_backbone("r18", pretrained=False)
+            net.fc = Identity()
+            net.apply(deactivate_batchnorm)
+            net = net.to(cuda).eval().to(memory_format=torch.channels_last)
+            x = torch.rand(6, 3, 80, 80, device=cuda, generator=torch.Generator(device=cuda).manual_seed(1))
+            with torch.no_grad():
+                outs.append(net(x.contiguous(memory_format=torch.channels_last)))
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop("MCGMIL_FUSE_INPUT_BN", None)
+    assert torch.equal(outs[0], outs[1])
