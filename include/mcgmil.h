@@ -126,8 +126,8 @@ int mcgmil_mcdo_forward(const mcgmil_args* a, void* stream);
 
 /* Its stages (same args/workspace; call in this order, after packing if packed_w is NULL):
  * mcgmil_gate_softmax_pool, then mcgmil_bag_stats. mcgmil_gate_softmax_pool is
- * ONE fused launch (gate scores, softmax, pooling) for batches of equal-size bags with >= 16,384
- * regions, else
+ * ONE fused launch (gate scores, softmax, pooling) for bf16 batches of equal-size bags with
+ * >= 16,384 regions, else
  * mcgmil_gate_scores followed by mcgmil_softmax_pool. MCGMIL_FUSED=1 takes the fused launch
  * whenever it applies, MCGMIL_FUSED=0 never (default: auto). Both give bitwise the same A and Y. */
 int mcgmil_gate_softmax_pool(const mcgmil_args* a, void* stream);

@@ -282,9 +282,10 @@ int try_fused_maxc(const mcgmil::GateParams& gp, long long total_rows, int L, hi
     }
     const int fm = fused_mode();
     if (fm == 0) return 0;
-    // auto: uniform batches only -- on ragged ones (config 4) the fused launch measured 2.8% slower
-    // (regions of 16-32 tiles straddling t-groups; profiles/r03/bench_cfg4*.log)
-    if (fm < 0 && (gp.uniform_rows <= 0 ||
+    // auto: bf16 uniform batches only -- on ragged ones (config 4) the fused launch measured 2.8%
+    // slower (regions of 16-32 tiles straddling t-groups; profiles/r03/bench_cfg4*.log), and in fp32
+    // (which spills in the tile loop) 13-18% slower (profiles/r03/probe_fused_f32.log)
+    if (fm < 0 && (sizeof(E) != 2 || gp.uniform_rows <= 0 ||
                    mcgmil_detail::fused_regions(gp, total_rows, mcgmil::fused_cap<MAXC>(), true) <
                        kFusedMinRegions))
         return 0;

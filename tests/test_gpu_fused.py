@@ -99,9 +99,10 @@ def test_fused_equals_two_kernel_path(cuda, case):
 
 
 def test_fused_auto_policy(cuda):
-    """MCGMIL_FUSED=auto (also the default, unset) takes the fused launch only for batches of
+    """MCGMIL_FUSED=auto (also the default, unset) takes the fused launch only for bf16 batches of
     equal-size bags with >= 16,384 regions: 16 bags of N=2048, T=100 (800 regions of two t-groups)
-    do not, 512 bags (25,600, the bench's step) do, ragged batches do not. MCGMIL_FUSED=0: never."""
+    do not, 512 bags (25,600, the bench's step) do, ragged or fp32 batches do not. MCGMIL_FUSED=0:
+    never."""
     from mcgmil import ops
     sd = synthetic.head_state_dict(0, C=2, shared=False)
     head = head_on(synthetic.head_arrays(sd, 2, False), cuda)
@@ -127,6 +128,13 @@ def test_fused_auto_policy(cuda):
         assert regions(big, ragged_offs, head, 100) == 0
     with fused("1"):
         assert regions(big, ragged_offs, head, 100) > 16384
+    # fp32 stays on the two-kernel path under auto (the fused fp32 tile loop spills: 13-18% slower)
+    big32 = torch.zeros(1280 * 512, 512, device=cuda, dtype=torch.float32)   # 1280 bags x 13 regions
+    offs32 = ops.bag_offsets_tensor([512] * 1280, cuda)
+    with fused("auto"):
+        assert regions(big32, offs32, head, 100) == 0
+    with fused("1"):
+        assert regions(big32, offs32, head, 100) == 1280 * 13
 
 
 from test_gpu_parity import BF16_CASES, FP32_CASES, TOL32, TOL_BF16_IN, compare, run  # noqa: E402
