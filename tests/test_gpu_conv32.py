@@ -120,6 +120,7 @@ def _combine(part):
 # (N, Cin, H, W, Cout, k, stride, pad): both tile shapes (Cout 64: 64 x 256, else 128 x 128), a
 # last pixel tile that is partly empty, the gather-mode stem, a 1x1 stride-2 downsample
 STATS_SHAPES = [
+    (1, 64, 3, 3, 64, 3, 1, 1),          # 9 pixels: three of the tile's four waves have none
     (3, 64, 20, 20, 64, 3, 1, 1),
     (2, 64, 17, 13, 128, 3, 2, 1),
     (2, 3, 40, 36, 64, 7, 2, 3),
@@ -218,3 +219,28 @@ def test_backbone_f32_input_bn_bitwise(cuda):
         finally:
             os.environ.pop("MCGMIL_FUSE_INPUT_BN", None)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("parts", [1, 1024, 1025, 3000])
+def test_bn_partials_combination(cuda, parts):
+    """(count, mean, M2) blocks -> BatchNorm coefficients, directly (<= 1024 blocks) or through the
+    chunked pre-combination (more): a_c, b_c match the fp64 combination of the same blocks."""
+    from mcgmil.features import batchnorm_coefficients
+    C = 64
+    g = torch.Generator(device=cuda).manual_seed(parts)
+    cnt = torch.randint(1, 300, (parts, 1), device=cuda, generator=g).float().expand(parts, C)
+    mean = torch.randn(parts, C, device=cuda, generator=g) * 0.5 + 3.0
+    M2 = (torch.rand(parts, C, device=cuda, generator=g) + 0.1) * cnt
+    part = torch.stack([cnt, mean, M2], 1).contiguous()
+    bn = nn.BatchNorm2d(C, track_running_stats=False).to(cuda).eval()
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, device=cuda, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, device=cuda, generator=g))
+    y = torch.zeros(8, C, 1, 1, device=cuda).contiguous(memory_format=torch.channels_last)   # not read
+    with torch.no_grad():
+        ab = batchnorm_coefficients(y, bn, part).double()
+    _, m, var = _combine(part)
+    a_ref = bn.weight.detach().double() / torch.sqrt(var + bn.eps)
+    b_ref = bn.bias.detach().double() - m * a_ref
+    assert float(((ab[0] - a_ref).abs() / a_ref.abs()).max()) <= 2e-6
+    assert float((ab[1] - b_ref).abs().max()) <= 2e-6 * float(b_ref.abs().max() + a_ref.abs().max() * m.abs().max())
