@@ -18,6 +18,7 @@ dropout RNG) on a bounded sample of the same workload on this host.
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import time
@@ -131,15 +132,20 @@ def main():
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--shared", type=int, default=0)
-    ap.add_argument("--workload", choices=["cfg3", "cfg4", "cfg5"], default="cfg3",
+    ap.add_argument("--workload", choices=["cfg3", "cfg4", "cfg5", "single"], default="cfg3",
                     help="cfg3: --bags bags of N=--n per GPU (weak scaling, the headline); "
                          "cfg4: 4096 bags N~U(256,2048) LPT-sharded over the GPUs (strong scaling); "
-                         "cfg5: end-to-end image -> patcher -> ResNet-18 -> head -> maps (bench_cfg5.py)")
+                         "cfg5: end-to-end image -> patcher -> ResNet-18 -> head -> maps (bench_cfg5.py); "
+                         "single: one bag per call through the drop-in module (infer.py:187-191)")
     ap.add_argument("--features", choices=["bf16", "fp32"], default="bf16",
                     help="cfg5 only: precision of the instances / ResNet / head operands")
     ap.add_argument("--dist-backend", default="nccl", help=argparse.SUPPRESS)   # rehearsal: gloo
     ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)  # ranks on cuda:0
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--busy-seconds", type=float, default=12.0,
+                    help="keep stepping (untimed) after the warm-up until the GPU has been busy this long")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the fp32 reference-precision and single-bag lines")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -167,14 +173,16 @@ def main():
             dist.destroy_process_group()
         return 0
 
-    from mcgmil import _lib, ops
-    from mcgmil import synthetic
-    lib = _lib.load()
+    from mcgmil import _lib
+
+    _lib.load()
+    if args.workload == "single":
+        out = single_bag_line(args, dev)
+        print(json.dumps(out))
+        return 0
 
     N, T, L, D, C = args.n, args.T, 512, 128, 2
     G = 1 if args.shared else C
-    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    esize = 2 if args.dtype == "bf16" else 4
     if args.workload == "cfg4":
         # BASELINE config 4: 4096 bags, N_b = rng(0).integers(256, 2049, 4096), sharded LPT
         import numpy as np
@@ -188,20 +196,98 @@ def main():
         sizes = [N] * args.bags
         ids = list(range(rank * args.bags, (rank + 1) * args.bags))
         total_bags = world * args.bags
-    B = len(sizes)
-    rows = sum(sizes)
 
-    # synthetic, random-init weights of the reference architecture; features |N(0,1)|
-    sd = synthetic.head_state_dict(0, L=L, D=D, C=C, shared=bool(args.shared))
-    arrays = synthetic.head_arrays(sd, C, bool(args.shared))
-    head = ops.HeadTensors(*[torch.from_numpy(arrays[k]).to(dev) for k in ops.HeadTensors._fields])
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    # headline: W warm-up steps, then untimed steps until the GPU has been busy --busy-seconds
+    # (the driver's utilisation sampler polls every few seconds), then K timed steps
+    r = measure_batch(sizes, ids, T, args.dtype, bool(args.shared), dev, world, args.steps,
+                      args.warmup, busy_s=args.busy_seconds, gather=True, seed_rank=rank)
+    el, gate_ms, fused, nreg, nbytes_packed = r["el"], r["gate_ms"], r["fused"], r["regions"], r["packed_bytes"]
+    esize = 2 if args.dtype == "bf16" else 4
+    total_bag_samples = total_bags * T * args.steps
+    value = total_bag_samples / el
+    F = sum(flops_per_bag(n, T, L, D, C, G) for n in sizes)
+    achieved = F / (gate_ms * 1e-3) / 1e12
+    hbm_bytes = sum(bytes_per_bag(n, T, L, C, esize) for n in sizes) + nbytes_packed
+    hbm_gbs = hbm_bytes / (gate_ms * 1e-3) / 1e9
+    traffic, traffic_src = measured_traffic(N, T, len(sizes), args.dtype, args.shared, "fused" if fused else "pipe") \
+        if args.workload == "cfg3" else (None, None)
+
+    # the reference's precision at the metric's shape (model.py:280-316 computes in fp32), and the
+    # one-bag-per-call caller (infer.py:187-191): N = 1 only, after the headline's timed steps
+    fp32_line = single = None
+    if world == 1 and args.workload == "cfg3" and not args.no_secondary:
+        fp32_line = fp32_secondary(args, dev)
+        single = single_bag_line(args, dev, quiet=True)
+
+    if rank == 0:
+        # the CPU baseline is a rank-0, N=1 figure: at N > 1 it would only hold the other ranks
+        cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(N, T, L, D, C, bool(args.shared),
+                                                                          args.cpu_budget)
+        kernel = (f"gate_fused_kernel (gate scores + softmax + pooling, one launch, {nreg} regions)"
+                  if fused else "gate_pipe_kernel")
+        out = {
+            "metric": METRIC, "value": value, "unit": "bag-samples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "weak" if args.workload == "cfg3" else "strong",
+            "vs_baseline": None,
+            "dtype": args.dtype, "data": "synthetic (|N(0,1)| features, random-init head)",
+            "config": {"workload": (f"BASELINE config 3: N={N} instances/bag" if args.workload == "cfg3"
+                                    else "BASELINE config 4: 4096 bags, N~U(256,2048)") +
+                                   f", d={L}, D={D}, C={C}, T={T} MCDO samples, "
+                                   f"{'shared' if args.shared else 'separate'} attention, "
+                                   f"{args.dtype} operands / fp32 accumulate",
+                       "bags_per_gpu_per_step": len(sizes), "global_batch_bags": total_bags,
+                       "rows_per_gpu": sum(sizes), "N": N if args.workload == "cfg3" else "U(256,2048)",
+                       "L": L, "D": D, "C": C, "T": T,
+                       "parallelism": f"bags over {world} GPU(s), LPT, RCCL all_gather of Y"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[args.dtype],
+                         "unit": "TFLOP/s", "frac": achieved / PEAK_TFLOPS[args.dtype],
+                         "traffic": traffic, "traffic_unit": "HBM bytes per launch",
+                         "traffic_source": traffic_src, "kernel": kernel,
+                         # what the HIP events bracket: the whole path (gate scores + softmax +
+                         # pooling) when fused, the gate GEMM kernel alone otherwise
+                         "timed_path": "fused: gate+softmax+pooling" if fused else "two-kernel: gate only",
+                         "kernel_ms": gate_ms, "algorithmic_tflop_per_launch": F / 1e12},
+            "roofline_hbm": {"achieved": hbm_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": hbm_gbs / PEAK_HBM_GBS,
+                             "algorithmic_bytes_per_launch": hbm_bytes},
+            "busy_warmup_s": r["busy_s"],
+            "fp32_reference_precision": fp32_line,
+            "single_bag": single,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+def _head(dev, shared, L=512, D=128, C=2):
+    from mcgmil import ops, synthetic
+    sd = synthetic.head_state_dict(0, L=L, D=D, C=C, shared=shared)
+    arrays = synthetic.head_arrays(sd, C, shared)
+    return ops.HeadTensors(*[torch.from_numpy(arrays[k]).to(dev) for k in ops.HeadTensors._fields])
+
+
+def measure_batch(sizes, ids, T, dtype, shared, dev, world, steps, warmup, busy_s=0.0, gather=False,
+                  seed_rank=0, path="auto"):
+    """Time `steps` passes of the hot path over one batch of bags resident in HBM: the gate
+    launch(es) through the C ABI, per-bag statistics, and (N > 1 GPUs, gather) the all_gather of
+    Y. HIP events on the launch stream bracket the gate kernel (the fused launch when it runs).
+    Returns wall seconds (max over ranks), the events' mean ms, the launch path."""
+    from mcgmil import _lib, ops
+    lib = _lib.load()
+    L, D, C = 512, 128, 2
+    G = 1 if shared else C
+    dt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    B, rows = len(sizes), sum(sizes)
+    head = _head(dev, shared)
+    g = torch.Generator(device=dev).manual_seed(1000 + seed_rank)
     H = torch.randn(rows, L, device=dev, generator=g).abs_().to(dt).contiguous()
     offs = ops.bag_offsets_tensor(sizes, dev)
     bag_ids = torch.tensor(ids, dtype=torch.int32, device=dev)
     packed = ops.packed_weights(head, dt)
-
-    a = ops.make_args(H, offs, head, T, C, G, D, 0.1, 0.1, seed=42, bag_ids=bag_ids)
+    a = ops.make_args(H, offs, head, T, C, G, D, 0.1, 0.1, seed=42, bag_ids=bag_ids, path=path)
     a.packed_w = ctypes.c_void_p(packed.data_ptr())
     Y = torch.empty(B, T, C, device=dev)
     A = torch.empty(T * C * rows, device=dev)
@@ -216,13 +302,12 @@ def main():
     pa = ctypes.byref(a)
     stream = torch.cuda.current_stream(dev)
     sh = ctypes.c_void_p(stream.cuda_stream)
-    if world > 1:
+    gat = None
+    if gather and world > 1:
         pad = torch.zeros(1, dtype=torch.int64, device=dev) + B
         dist.all_reduce(pad, op=dist.ReduceOp.MAX)
         Ypad = torch.zeros(int(pad), T, C, device=dev)
-        gather = [torch.empty_like(Ypad) for _ in range(world)]
-    else:
-        gather = None
+        gat = [torch.empty_like(Ypad) for _ in range(world)]
 
     # ONE launch (gate_fused_kernel: gate scores + softmax + pooling) when the batch is large
     # enough, else gate_pipe_kernel + softmax_pool_kernel; the events bracket the gate kernel
@@ -242,74 +327,133 @@ def main():
         if not fused:
             _lib.check(lib.mcgmil_softmax_pool(pa, sh), "softmax_pool")
         _lib.check(lib.mcgmil_bag_stats(pa, sh), "bag_stats")
-        if gather is not None:       # per-bag predictions to every rank (RCCL over xGMI)
+        if gat is not None:          # per-bag predictions to every rank (RCCL over xGMI)
             Ypad[:B].copy_(Y)
-            dist.all_gather(gather, Ypad)
+            dist.all_gather(gat, Ypad)
 
-    for _ in range(args.warmup):
+    t_busy = time.perf_counter()
+    for _ in range(warmup):
         step()
+    extra = 0
+    if busy_s > 0:
+        # untimed steps until the GPU has been busy busy_s seconds; the count is agreed over the
+        # ranks (each step ends in a collective)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        per = (time.perf_counter() - t1) / 2
+        extra = max(0, math.ceil((busy_s - (time.perf_counter() - t_busy)) / max(per, 1e-4)))
+        if world > 1:
+            t = torch.tensor([extra], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            extra = int(t)
+        for _ in range(extra):
+            step()
+    torch.cuda.synchronize()
+    busy = time.perf_counter() - t_busy
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+           for _ in range(steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         step(evs[i])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    gate_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / args.steps
+    gate_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / steps
     if world > 1:
         t = torch.tensor([el, gate_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, gate_ms = float(t[0]), float(t[1])
+    return {"el": el, "gate_ms": gate_ms, "fused": fused, "regions": regions.value,
+            "packed_bytes": packed.numel(), "busy_s": busy, "busy_extra_steps": extra}
 
-    total_bag_samples = total_bags * T * args.steps
-    value = total_bag_samples / el
-    F = sum(flops_per_bag(n, T, L, D, C, G) for n in sizes)
-    achieved = F / (gate_ms * 1e-3) / 1e12
-    hbm_bytes = sum(bytes_per_bag(n, T, L, C, esize) for n in sizes) + packed.numel()
-    hbm_gbs = hbm_bytes / (gate_ms * 1e-3) / 1e9
-    traffic, traffic_src = measured_traffic(N, T, B, args.dtype, args.shared, "fused" if fused else "pipe") \
-        if args.workload == "cfg3" else (None, None)
-    if rank == 0:
-        # the CPU baseline is a rank-0, N=1 figure: at N > 1 it would only hold the other ranks
-        cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(N, T, L, D, C, bool(args.shared),
-                                                                          args.cpu_budget)
-        out = {
-            "metric": METRIC, "value": value, "unit": "bag-samples/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps,
-            "higher_is_better": True, "scaling": "weak" if args.workload == "cfg3" else "strong",
-            "vs_baseline": None,
-            "dtype": args.dtype, "data": "synthetic (|N(0,1)| features, random-init head)",
-            "config": {"workload": (f"BASELINE config 3: N={N} instances/bag" if args.workload == "cfg3"
-                                    else "BASELINE config 4: 4096 bags, N~U(256,2048)") +
-                                   f", d={L}, D={D}, C={C}, T={T} MCDO samples, "
-                                   f"{'shared' if args.shared else 'separate'} attention, "
-                                   f"{args.dtype} operands / fp32 accumulate",
-                       "bags_per_gpu_per_step": B, "global_batch_bags": total_bags,
-                       "rows_per_gpu": rows, "N": N if args.workload == "cfg3" else "U(256,2048)",
-                       "L": L, "D": D, "C": C, "T": T,
-                       "parallelism": f"bags over {world} GPU(s), LPT, RCCL all_gather of Y"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[args.dtype],
-                         "unit": "TFLOP/s", "frac": achieved / PEAK_TFLOPS[args.dtype],
-                         "traffic": traffic, "traffic_unit": "HBM bytes per launch",
-                         "traffic_source": traffic_src,
-                         "kernel": (f"gate_fused_kernel (gate scores + softmax + pooling, one launch, "
-                                    f"{regions.value} regions)" if fused else "gate_pipe_kernel"),
-                         "kernel_ms": gate_ms, "algorithmic_tflop_per_launch": F / 1e12},
-            "roofline_hbm": {"achieved": hbm_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": hbm_gbs / PEAK_HBM_GBS,
-                             "algorithmic_bytes_per_launch": hbm_bytes},
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(out))
-    if world > 1:
-        dist.destroy_process_group()
-    return 0
+
+def fp32_secondary(args, dev, bags=64, steps=10, warmup=2):
+    """The same hot path at the reference's precision (fp32 operands and accumulation, model.py:
+    280-316): `bags` bags of N=--n, T=--T, separate heads, priced against the fp32 MFMA peak."""
+    N, T, L, D, C = args.n, args.T, 512, 128, 2
+    r = measure_batch([N] * bags, list(range(bags)), T, "f32", False, dev, 1, steps, warmup)
+    F = bags * flops_per_bag(N, T, L, D, C, C)
+    ach = F / (r["gate_ms"] * 1e-3) / 1e12
+    return {"metric": "bag-samples/s, fp32 operands (the reference precision)",
+            "value": bags * T * steps / r["el"], "unit": "bag-samples/s", "dtype": "f32",
+            "steps": steps, "warmup": warmup, "ms_per_step": r["el"] * 1e3 / steps,
+            "config": f"{bags} bags of N={N}, d={L}, D={D}, C={C}, T={T}, separate attention, fp32",
+            "roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_TFLOPS["f32"], "unit": "TFLOP/s",
+                         "frac": ach / PEAK_TFLOPS["f32"], "kernel_ms": r["gate_ms"],
+                         "kernel": (f"gate_fused_kernel ({r['regions']} regions)" if r["fused"]
+                                    else "gate_pipe_kernel (fp32 MFMA 16x16x4)"),
+                         "timed_path": "fused: gate+softmax+pooling" if r["fused"] else "two-kernel: gate only",
+                         "algorithmic_tflop_per_launch": F / 1e12}}
+
+
+def single_bag_line(args, dev, quiet=False):
+    """The per-bag caller (infer.py:187-191 calls mc_inference once per bag): the drop-in module's
+    mc_inference_features on ONE bag per call, N = --n (and config 5's k = 1,507), T = --T, bf16
+    operands, separate heads, A_mean/A_var/P_mean included. Reports
+      gpu_ms   device time per call: events around a run of calls queued behind a busy GPU, so
+               host overhead is hidden and only kernels + on-device launch gaps count;
+      host_ms  host time per call (the Python/ctypes path, no synchronisation);
+      sync_ms  one call from an idle GPU to its results on the host side (latency).
+    """
+    from mcgmil import MultiHeadGatedAttentionMIL, synthetic
+    L, D, C, T = 512, 128, 2, args.T
+    m = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=False)
+    sd = synthetic.head_state_dict(0, L=L, D=D, C=C, shared=False)
+    own = m.state_dict()
+    m.load_state_dict({k: torch.from_numpy(v).reshape(own[k].shape) for k, v in sd.items()}, strict=False)
+    m.compute_dtype = torch.bfloat16
+    m = m.to(dev).eval()
+    res = {}
+    for N in (args.n, 1507):
+        g = torch.Generator(device=dev).manual_seed(7)
+        H = torch.randn(N, L, device=dev, generator=g).abs_().bfloat16()
+        call = lambda i: m.mc_inference_features(H, T=T, seed=100 + i, return_stats=True)  # noqa: E731
+        for i in range(5):
+            call(i)
+        torch.cuda.synchronize()
+        reps = 50
+        # host time per call, nothing queued
+        t0 = time.perf_counter()
+        for i in range(reps):
+            call(i)
+        host = (time.perf_counter() - t0) / reps
+        torch.cuda.synchronize()
+        # device time per call: a busy kernel queued ahead (~0.1 s), so the host enqueues every
+        # call before the GPU reaches them
+        torch.cuda._sleep(int(2e8))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s = torch.cuda.current_stream(dev)
+        e0.record(s)
+        for i in range(reps):
+            call(i)
+        e1.record(s)
+        torch.cuda.synchronize()
+        gpu = e0.elapsed_time(e1) / reps
+        lat = []
+        for i in range(10):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            call(i)
+            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - t0)
+        F = flops_per_bag(N, T, L, D, C, C)
+        ach = F / (gpu * 1e-3) / 1e12
+        res[f"N{N}"] = {"gpu_ms": gpu, "host_ms": host * 1e3, "sync_ms": sorted(lat)[len(lat) // 2] * 1e3,
+                        "achieved_tflops": ach, "frac": ach / PEAK_TFLOPS["bf16"],
+                        "bag_samples_per_s": T / (gpu * 1e-3)}
+    out = {"metric": "one bag per call (infer.py:187-191): head device time per bag",
+           "unit": "ms", "dtype": "bf16", "T": T, "bags": res,
+           "path": "MultiHeadGatedAttentionMIL.mc_inference_features -> mcgmil_mcdo_forward "
+                   "(two-kernel path + bag statistics)"}
+    return out
 
 
 if __name__ == "__main__":

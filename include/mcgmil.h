@@ -20,7 +20,7 @@
  *                            for the kernel once per model
  *   mcgmil_gate_softmax_pool
  *                         <- model.py:280-316 for all T samples: the two stages below, or ONE
- *                            fused launch (MCGMIL_FUSED); A and Y are bitwise the same either way
+ *                            fused launch (args->flags); A and Y are bitwise the same either way
  *   mcgmil_gate_scores / mcgmil_softmax_pool / mcgmil_bag_stats
  *                         <- the stages of mcgmil_mcdo_forward, exposed for profiling
  *   mcgmil_feature_keep / mcgmil_attention_keep
@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define MCGMIL_ABI_VERSION 1
+#define MCGMIL_ABI_VERSION 2   /* 2: mcgmil_args.flags (path selection) */
 
 enum mcgmil_status {
     MCGMIL_OK = 0,
@@ -59,6 +59,24 @@ enum mcgmil_status {
 };
 
 enum mcgmil_dtype { MCGMIL_F32 = 0, MCGMIL_BF16 = 1 };
+
+/* mcgmil_args.flags: which launch path mcgmil_gate_softmax_pool / mcgmil_mcdo_forward take. All
+ * paths give bitwise the same A and Y (tests/test_gpu_fused.py); the choice is performance only.
+ * The environment variables MCGMIL_FUSED (0 | 1 | auto) and MCGMIL_GATE (pipe | pp), when set,
+ * override the flags (A/B timing of an unmodified caller). */
+enum mcgmil_flags {
+    MCGMIL_PATH_AUTO = 0,        /* fused launch for bf16 batches of equal-size bags with >= 16,384
+                                    regions, else the two kernels */
+    MCGMIL_PATH_FUSED = 1,       /* the fused launch whenever it applies (bf16 or fp32, L % 64 == 0,
+                                    <= 16 gate tile pairs, no replay masks) */
+    MCGMIL_PATH_TWO_KERNEL = 2,  /* never fused: gate scores -> workspace -> softmax/pooling */
+    MCGMIL_PATH_MASK = 3,
+    MCGMIL_GATE_AUTO = 0 << 2,   /* two-kernel path, bf16 heads: gate_pipe_kernel for > 8 gate tile
+                                    pairs (separate heads), gate_pp_kernel for <= 8 (shared) */
+    MCGMIL_GATE_PIPE = 1 << 2,   /* always gate_pipe_kernel (one 8-wave workgroup per CU) */
+    MCGMIL_GATE_PP = 2 << 2,     /* gate_pp_kernel (two 4-wave workgroups per CU) where it applies */
+    MCGMIL_GATE_MASK = 3 << 2
+};
 
 typedef struct mcgmil_args {
     /* ---- sizes ---- */
@@ -108,6 +126,9 @@ typedef struct mcgmil_args {
     size_t workspace_bytes;
     void* debug;          /* diagnostic builds only (-DMCGMIL_STAMPS): per-tile s_memtime
                              stamps; ignored by the product build. NULL otherwise */
+    /* ---- policy ---- */
+    int32_t flags;        /* mcgmil_flags: MCGMIL_PATH_* | MCGMIL_GATE_* (0 = auto) */
+    int32_t reserved;     /* must be 0 */
 } mcgmil_args;
 
 int mcgmil_abi_version(void);
@@ -126,10 +147,9 @@ int mcgmil_mcdo_forward(const mcgmil_args* a, void* stream);
 
 /* Its stages (same args/workspace; call in this order, after packing if packed_w is NULL):
  * mcgmil_gate_softmax_pool, then mcgmil_bag_stats. mcgmil_gate_softmax_pool is
- * ONE fused launch (gate scores, softmax, pooling) for bf16 batches of equal-size bags with
- * >= 16,384 regions, else
- * mcgmil_gate_scores followed by mcgmil_softmax_pool. MCGMIL_FUSED=1 takes the fused launch
- * whenever it applies, MCGMIL_FUSED=0 never (default: auto). Both give bitwise the same A and Y. */
+ * ONE fused launch (gate scores, softmax, pooling) or mcgmil_gate_scores followed by
+ * mcgmil_softmax_pool, as args->flags selects (MCGMIL_PATH_*; default auto: fused for bf16
+ * batches of equal-size bags with >= 16,384 regions). Both give bitwise the same A and Y. */
 int mcgmil_gate_softmax_pool(const mcgmil_args* a, void* stream);
 /* The fused launch mcgmil_gate_softmax_pool would make for these args: *regions = its number of
  * workgroups (one per region of t-groups of a bag; an upper bound for ragged bags), or 0 when

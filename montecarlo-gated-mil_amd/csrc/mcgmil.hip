@@ -5,7 +5,9 @@
 #include <string.h>
 
 #include <mutex>
+#include <set>
 #include <string>
+#include <utility>
 
 #include "../../include/mcgmil.h"
 #include "mcgmil_error.h"
@@ -24,6 +26,20 @@ int fail(int code, const std::string& msg) {
 
 int hip_fail(hipError_t e, const char* what) {
     return fail(MCGMIL_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int raise_lds_limit(const void* k, const char* what) {
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, what);
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.count({k, dev})) return MCGMIL_OK;
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return hip_fail(e, what);
+    done.insert({k, dev});
+    return MCGMIL_OK;
 }
 
 }  // namespace mcgmil_detail
@@ -85,6 +101,9 @@ int validate_batch(const mcgmil_args* a) {
         return fail(MCGMIL_E_INVALID, "uniform_bag_rows must be 0 or total_rows / num_bags");
     if (!(a->p_feat >= 0.f && a->p_feat <= 1.f) || !(a->p_att >= 0.f && a->p_att <= 1.f))
         return fail(MCGMIL_E_INVALID, "dropout probabilities must be in [0, 1]");
+    if ((a->flags & ~(MCGMIL_PATH_MASK | MCGMIL_GATE_MASK)) != 0 || (a->flags & MCGMIL_PATH_MASK) == 3 ||
+        (a->flags & MCGMIL_GATE_MASK) == (3 << 2) || a->reserved != 0)
+        return fail(MCGMIL_E_INVALID, "flags must be MCGMIL_PATH_* | MCGMIL_GATE_* and reserved 0");
     return MCGMIL_OK;
 }
 
@@ -125,12 +144,6 @@ const void* packed_ptr(const mcgmil_args* a) {
     return a->packed_w ? a->packed_w : a->workspace;
 }
 
-template <typename KernelT>
-void raise_lds_cap(KernelT* k) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-}
-
 // The tile plan for BM-row tiles (written into the workspace; gp.tile_bag points there).
 int launch_plan(const mcgmil::GateParams& gp, int BM, hipStream_t s) {
     const long long tiles = (gp.total_samples + BM - 1) / BM;
@@ -145,8 +158,9 @@ int launch_plan(const mcgmil::GateParams& gp, int BM, hipStream_t s) {
 template <typename E, int BM, int PPW, int MAXC>
 int launch_gate_generic(const mcgmil::GateParams& gp, hipStream_t s) {
     auto* k = &mcgmil::gate_scores_kernel<E, BM, PPW, MAXC>;
-    static std::once_flag once;   // per instantiation: all scratch is dynamic LDS (> 64 KiB)
-    std::call_once(once, [&] { raise_lds_cap(k); });
+    // all scratch is dynamic LDS (> 64 KiB)
+    if (int rc = mcgmil_detail::raise_lds_limit(reinterpret_cast<const void*>(k), "gate_scores_kernel LDS limit"))
+        return rc;
     const long long tiles = (gp.total_samples + BM - 1) / BM;
     if (tiles == 0) return MCGMIL_OK;
     if (gp.uniform_rows <= 0)
@@ -160,8 +174,8 @@ int launch_gate_generic(const mcgmil::GateParams& gp, hipStream_t s) {
 template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE>
 int launch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
     auto* k = &mcgmil::gate_pipe_kernel<E, PPW, MAXC, REPLAY, ONE>;
-    static std::once_flag once;
-    std::call_once(once, [&] { raise_lds_cap(k); });
+    if (int rc = mcgmil_detail::raise_lds_limit(reinterpret_cast<const void*>(k), "gate_pipe_kernel LDS limit"))
+        return rc;
     const long long tiles = (gp.total_samples + mcgmil::kPipeBM - 1) / mcgmil::kPipeBM;
     if (tiles == 0) return MCGMIL_OK;
     if (gp.uniform_rows <= 0)
@@ -189,19 +203,22 @@ int launch_gate_pp(const mcgmil::GateParams& gp, hipStream_t s) {
 // Kernel choice for bf16 heads of up to 16 gate tile pairs (measured, config 3, MI355X):
 // separate heads (P = 16) run the one-workgroup-per-CU gate_pipe_kernel (914 vs 853 TFLOP/s),
 // shared heads (P = 8) the two-workgroups-per-CU gate_pp_kernel (820 vs 781).
-// MCGMIL_GATE=pipe / pp forces one of them (A/B timing). Variants measured slower and removed
-// are listed with their numbers in profiles/r02/gate_ab.log and DESIGN.md §5.
+// args->flags MCGMIL_GATE_PIPE / _PP force one of them; MCGMIL_GATE=pipe / pp in the environment
+// overrides the flags (A/B timing). Variants measured slower and removed are listed with their
+// numbers in profiles/r02/gate_ab.log and DESIGN.md §5.
 #ifndef MCGMIL_GATE_DEFAULT
 #define MCGMIL_GATE_DEFAULT 0       // A/B builds: 1 pipe, 2 pp
 #endif
-int gate_mode() {   // 0 auto, 1 pipe, 2 pp
-    static const int mode = [] {
+int gate_mode(int flags) {   // 0 auto, 1 pipe, 2 pp
+    static const int env = [] {
         const char* e = getenv("MCGMIL_GATE");
         if (e && strcmp(e, "pipe") == 0) return 1;
         if (e && strcmp(e, "pp") == 0) return 2;
-        return MCGMIL_GATE_DEFAULT;
+        return -1;
     }();
-    return mode;
+    if (env >= 0) return env;
+    const int f = (flags & MCGMIL_GATE_MASK) >> 2;
+    return f ? f : MCGMIL_GATE_DEFAULT;
 }
 
 template <int RT, int PPW, int MAXC>
@@ -226,10 +243,10 @@ int dispatch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
 }
 
 template <typename E, int MAXC>
-int dispatch_gate_maxc(const mcgmil::GateParams& gp, int L, int dtype, hipStream_t s) {
+int dispatch_gate_maxc(const mcgmil::GateParams& gp, int L, int dtype, int flags, hipStream_t s) {
     const bool pipe_ok = L % 64 == 0;          // the pipelined K loop is unrolled by two steps
     if constexpr (sizeof(E) == 2) {
-        const int mode = gate_mode();
+        const int mode = gate_mode(flags);
         if (pipe_ok && mode != 1) {
             if (gp.P <= 2 * mcgmil::kPPWaves) return dispatch_gate_pp<8, 2, MAXC>(gp, s);
             if (mode == 2 && gp.P <= 4 * mcgmil::kPPWaves) return dispatch_gate_pp<4, 4, MAXC>(gp, s);
@@ -244,9 +261,9 @@ int dispatch_gate_maxc(const mcgmil::GateParams& gp, int L, int dtype, hipStream
 }
 
 template <typename E>
-int dispatch_gate(const mcgmil::GateParams& gp, int L, int dtype, hipStream_t s) {
-    return gp.C <= 2 ? dispatch_gate_maxc<E, 2>(gp, L, dtype, s)
-                     : dispatch_gate_maxc<E, 4>(gp, L, dtype, s);
+int dispatch_gate(const mcgmil::GateParams& gp, int L, int dtype, int flags, hipStream_t s) {
+    return gp.C <= 2 ? dispatch_gate_maxc<E, 2>(gp, L, dtype, flags, s)
+                     : dispatch_gate_maxc<E, 4>(gp, L, dtype, flags, s);
 }
 
 // Fused single launch (gate_fused_kernel) or the two-kernel path (gate scores into the
@@ -255,32 +272,34 @@ int dispatch_gate(const mcgmil::GateParams& gp, int L, int dtype, hipStream_t s)
 // needs many regions to fill 256 CUs without a tail. By default (MCGMIL_FUSED unset or "auto")
 // it takes batches of equal-size bags with >= 16,384 regions (64 per CU): at config 3 it is 0.1-0.8% faster than the
 // two-kernel path in the same process (bitwise the same outputs) and moves 40% fewer
-// HBM bytes (no logits/z workspace round trip). MCGMIL_FUSED=1 takes it whenever it applies,
-// MCGMIL_FUSED=0 never.
+// HBM bytes (no logits/z workspace round trip). args->flags MCGMIL_PATH_FUSED takes it whenever it
+// applies, MCGMIL_PATH_TWO_KERNEL never; MCGMIL_FUSED=1 / 0 / auto in the environment overrides.
 constexpr long long kFusedMinRegions = 16384;
 
-int fused_mode() {   // -1 auto, 0 off, 1 on (read per call: tests switch it in one process)
+int fused_mode(int flags) {   // -1 auto, 0 off, 1 on (env read per call: tests switch it in one process)
     const char* e = getenv("MCGMIL_FUSED");
     if (e && strcmp(e, "1") == 0) return 1;
     if (e && strcmp(e, "0") == 0) return 0;
-    return -1;      // default: auto
+    if (e && strcmp(e, "auto") == 0) return -1;
+    const int path = flags & MCGMIL_PATH_MASK;
+    return path == MCGMIL_PATH_FUSED ? 1 : path == MCGMIL_PATH_TWO_KERNEL ? 0 : -1;
 }
 
 // Returns 1 if the fused kernel was launched (with `regions` set: nothing is launched, *regions
 // = its grid), 0 if the caller must run the two-kernel path.
 template <typename E, int MAXC>
-int try_fused_maxc(const mcgmil::GateParams& gp, long long total_rows, int L, hipStream_t s, int* rc,
-                   long long* regions = nullptr) {
+int try_fused_maxc(const mcgmil::GateParams& gp, long long total_rows, int L, int flags, hipStream_t s,
+                   int* rc, long long* regions = nullptr) {
     *rc = MCGMIL_OK;
     // (L >= 128: the fused pipeline peels two K steps at each end of a tile)
     if (gp.keep_feat || L % 64 != 0 || L < 128 || gp.P > 2 * mcgmil::kGateWaves) return 0;
     if (mcgmil::fused_kernel_lds_bytes<E, MAXC>(L) > 160 * 1024) return 0;   // bf16 L > 1024
     if constexpr (sizeof(E) == 2) {       // bf16: the kernel dispatch_gate_maxc would pick
-        const int mode = gate_mode();
+        const int mode = gate_mode(flags);
         const bool pipe = mode == 1 || (mode == 0 && gp.P > 2 * mcgmil::kPPWaves);
         if (!pipe) return 0;
     }
-    const int fm = fused_mode();
+    const int fm = fused_mode(flags);
     if (fm == 0) return 0;
     // auto: bf16 uniform batches only -- on ragged ones (config 4) the fused launch measured 2.8%
     // slower (regions of 16-32 tiles straddling t-groups; profiles/r03/bench_cfg4*.log), and in fp32
@@ -301,10 +320,10 @@ int try_fused_maxc(const mcgmil::GateParams& gp, long long total_rows, int L, hi
 }
 
 template <typename E>
-int try_fused(const mcgmil::GateParams& gp, long long total_rows, int L, hipStream_t s, int* rc,
+int try_fused(const mcgmil::GateParams& gp, long long total_rows, int L, int flags, hipStream_t s, int* rc,
               long long* regions = nullptr) {
-    return gp.C <= 2 ? try_fused_maxc<E, 2>(gp, total_rows, L, s, rc, regions)
-                     : try_fused_maxc<E, 4>(gp, total_rows, L, s, rc, regions);
+    return gp.C <= 2 ? try_fused_maxc<E, 2>(gp, total_rows, L, flags, s, rc, regions)
+                     : try_fused_maxc<E, 4>(gp, total_rows, L, flags, s, rc, regions);
 }
 
 }  // namespace
@@ -425,8 +444,8 @@ int mcgmil_gate_scores(const mcgmil_args* a, void* stream) {
     mcgmil::GateParams gp;
     if (int rc = gate_params(a, gp)) return rc;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (a->h_dtype == MCGMIL_BF16) return dispatch_gate<__bf16>(gp, a->L, a->h_dtype, s);
-    return dispatch_gate<float>(gp, a->L, a->h_dtype, s);
+    if (a->h_dtype == MCGMIL_BF16) return dispatch_gate<__bf16>(gp, a->L, a->h_dtype, a->flags, s);
+    return dispatch_gate<float>(gp, a->L, a->h_dtype, a->flags, s);
 }
 
 int mcgmil_fused_regions(const mcgmil_args* a, int64_t* regions) {
@@ -435,8 +454,8 @@ int mcgmil_fused_regions(const mcgmil_args* a, int64_t* regions) {
     if (int rc = gate_params(a, gp)) return rc;
     int rc = MCGMIL_OK;
     long long r = 0;
-    const int fused = a->h_dtype == MCGMIL_BF16 ? try_fused<__bf16>(gp, a->total_rows, a->L, nullptr, &rc, &r)
-                                                : try_fused<float>(gp, a->total_rows, a->L, nullptr, &rc, &r);
+    const int fused = a->h_dtype == MCGMIL_BF16 ? try_fused<__bf16>(gp, a->total_rows, a->L, a->flags, nullptr, &rc, &r)
+                                                : try_fused<float>(gp, a->total_rows, a->L, a->flags, nullptr, &rc, &r);
     *regions = fused ? r : 0;
     return MCGMIL_OK;
 }
@@ -447,8 +466,8 @@ int mcgmil_gate_softmax_pool(const mcgmil_args* a, void* stream) {
     if (!a->Y) return fail(MCGMIL_E_INVALID, "Y is NULL");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc = MCGMIL_OK;
-    const int fused = a->h_dtype == MCGMIL_BF16 ? try_fused<__bf16>(gp, a->total_rows, a->L, s, &rc)
-                                                : try_fused<float>(gp, a->total_rows, a->L, s, &rc);
+    const int fused = a->h_dtype == MCGMIL_BF16 ? try_fused<__bf16>(gp, a->total_rows, a->L, a->flags, s, &rc)
+                                                : try_fused<float>(gp, a->total_rows, a->L, a->flags, s, &rc);
     if (fused) return rc;
     if ((rc = mcgmil_gate_scores(a, stream))) return rc;
     return mcgmil_softmax_pool(a, stream);

@@ -978,57 +978,35 @@ Plan make_plan(ConvGeom& g) {
     return p;
 }
 
-template <typename K>
-void raise_lds(K k) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+// Launch k after raising its dynamic-LDS limit (once per kernel and device; errors returned).
+template <typename K, typename A>
+int launch_lds(K k, dim3 grid, dim3 block, size_t lds, hipStream_t s, const A& arg) {
+    if (int rc = mcgmil_detail::raise_lds_limit(reinterpret_cast<const void*>(k), "convolution kernel LDS limit"))
+        return rc;
+    hipLaunchKernelGGL(k, grid, block, lds, s, arg);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "convolution kernel launch");
 }
 
 int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
-    static std::once_flag once;
-    std::call_once(once, [] {
-        raise_lds(conv_dma_kernel<256, 128, 4, 3, false>);
-        raise_lds(conv_dma_kernel<256, 128, 4, 3, true>);
-        raise_lds(conv_dma_kernel<256, 64, 4, 3, false>);
-        raise_lds(conv_dma_kernel<256, 64, 4, 3, true>);
-        raise_lds(conv_dma_kernel<512, 128, 4, 2, false>);
-        raise_lds(conv_dma_kernel<256, 256, 2, 2, false>);
-        raise_lds(conv3x3c64_kernel<false, false>);
-        raise_lds(conv3x3c64_kernel<true, false>);
-        raise_lds(conv3x3c64_kernel<false, true>);
-        raise_lds(conv3x3c64_kernel<true, true>);
-        raise_lds(conv3x3_halo_kernel<false, false>);
-        raise_lds(conv3x3_halo_kernel<true, false>);
-        raise_lds(conv3x3_halo_kernel<false, true>);
-        raise_lds(conv3x3_halo_kernel<true, true>);
-    });
     const bool stats = g.stats != nullptr, xf = g.in_ab != nullptr;
     const dim3 grid((unsigned)p.grid), block(kThreads);
-    if (p.kind == 1) {
+    if (p.kind == 1 || p.kind == 4) {
         HaloGeom hg = p.hg;
         hg.g = g;
-        auto k = stats ? (xf ? conv3x3c64_kernel<true, true> : conv3x3c64_kernel<true, false>)
-                       : (xf ? conv3x3c64_kernel<false, true> : conv3x3c64_kernel<false, false>);
-        hipLaunchKernelGGL(k, grid, block, p.lds, s, hg);
-    } else if (p.kind == 4) {
-        HaloGeom hg = p.hg;
-        hg.g = g;
-        auto k = stats ? (xf ? conv3x3_halo_kernel<true, true> : conv3x3_halo_kernel<true, false>)
-                       : (xf ? conv3x3_halo_kernel<false, true> : conv3x3_halo_kernel<false, false>);
-        hipLaunchKernelGGL(k, grid, block, p.lds, s, hg);
-    } else if (p.kind == 2) {
-        if (stats) hipLaunchKernelGGL((conv_dma_kernel<256, 128, 4, 3, true>), grid, block, p.lds, s, g);
-        else hipLaunchKernelGGL((conv_dma_kernel<256, 128, 4, 3, false>), grid, block, p.lds, s, g);
-    } else if (p.kind == 5) {
-        hipLaunchKernelGGL((conv_dma_kernel<512, 128, 4, 2, false>), grid, block, p.lds, s, g);
-    } else if (p.kind == 6) {
-        hipLaunchKernelGGL((conv_dma_kernel<256, 256, 2, 2, false>), grid, block, p.lds, s, g);
-    } else {
-        if (stats) hipLaunchKernelGGL((conv_dma_kernel<256, 64, 4, 3, true>), grid, block, p.lds, s, g);
-        else hipLaunchKernelGGL((conv_dma_kernel<256, 64, 4, 3, false>), grid, block, p.lds, s, g);
+        auto k = p.kind == 1 ? (stats ? (xf ? conv3x3c64_kernel<true, true> : conv3x3c64_kernel<true, false>)
+                                      : (xf ? conv3x3c64_kernel<false, true> : conv3x3c64_kernel<false, false>))
+                             : (stats ? (xf ? conv3x3_halo_kernel<true, true> : conv3x3_halo_kernel<true, false>)
+                                      : (xf ? conv3x3_halo_kernel<false, true> : conv3x3_halo_kernel<false, false>));
+        return launch_lds(k, grid, block, p.lds, s, hg);
     }
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "convolution kernel launch");
+    if (p.kind == 2)
+        return stats ? launch_lds(conv_dma_kernel<256, 128, 4, 3, true>, grid, block, p.lds, s, g)
+                     : launch_lds(conv_dma_kernel<256, 128, 4, 3, false>, grid, block, p.lds, s, g);
+    if (p.kind == 5) return launch_lds(conv_dma_kernel<512, 128, 4, 2, false>, grid, block, p.lds, s, g);
+    if (p.kind == 6) return launch_lds(conv_dma_kernel<256, 256, 2, 2, false>, grid, block, p.lds, s, g);
+    return stats ? launch_lds(conv_dma_kernel<256, 64, 4, 3, true>, grid, block, p.lds, s, g)
+                 : launch_lds(conv_dma_kernel<256, 64, 4, 3, false>, grid, block, p.lds, s, g);
 }
 
 // weights [Cout, Cin, KH, KW] (fp32 or bf16) -> [Cout, KH, KW, Cin] bf16

@@ -16,12 +16,13 @@ constexpr int kWave = 64;
 // ---------------------------------------------------------------------------------------
 // FLIP_XZ: output words x and z come out XORed with 0x80008000 (the sign flip of the packed
 // keep rule, drop_mask16x2_flipped) -- folded into the last round's key words, i.e. free.
-template <bool FLIP_XZ = false>
+// ROUNDS: 10 is the product stream (Random123's default); other counts exist for timing studies.
+template <bool FLIP_XZ = false, int ROUNDS = 10>
 __device__ __forceinline__ uint4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                uint32_t k0, uint32_t k1) {
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        if (FLIP_XZ && r == 9) {
+    for (int r = 0; r < ROUNDS; ++r) {
+        if (FLIP_XZ && r == ROUNDS - 1) {
             k0 ^= 0x80008000u;
             k1 ^= 0x80008000u;
         }

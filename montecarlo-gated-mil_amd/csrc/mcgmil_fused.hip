@@ -8,7 +8,6 @@
 #include "mcgmil_error.h"
 #include "mcgmil_fused.h"
 
-#include <mutex>
 
 namespace mcgmil {
 
@@ -60,11 +59,7 @@ namespace {
 template <typename E, int PPW, int MAXC, bool ONE>
 int launch(const mcgmil::GateParams& gp, long long total_rows, hipStream_t s) {
     auto* k = &mcgmil::gate_fused_kernel<E, PPW, MAXC, ONE>;
-    static std::once_flag once;
-    std::call_once(once, [&] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    });
+    if (int rc = raise_lds_limit(reinterpret_cast<const void*>(k), "gate_fused_kernel LDS limit")) return rc;
     constexpr int cap = mcgmil::fused_cap<MAXC>();
     if (gp.uniform_rows <= 0) {
         hipLaunchKernelGGL(mcgmil::plan_regions_kernel, dim3(1), dim3(1024), 0, s, gp.bag_off, gp.B,

@@ -153,6 +153,9 @@ __device__ __forceinline__ float gated_product_scaled(float ax, float by) {
 #ifndef MCGMIL_DIAG
 #define MCGMIL_DIAG 0               // ablation bits for timing studies (never in the product)
 #endif
+#ifndef MCGMIL_PHILOX_ROUNDS
+#define MCGMIL_PHILOX_ROUNDS 10     // feature-mask rounds in the pipelined K loop (timing studies only)
+#endif
 
 constexpr float kM2Log2e = -2.8853900817779268f;   // -2 / ln 2
 constexpr float kMLog2e = -1.4426950408889634f;    // -1 / ln 2
@@ -307,49 +310,6 @@ __device__ __forceinline__ void finish_scores(const GateParams& p, long long R0,
                               (uint32_t)n, p.thr_a);
     }
     // row R0 + r of the flattened (bag, t, n) space -> lg_out / z_out row R0 + r - obase
-    const size_t o = (size_t)(R0 + r - obase) * p.C + c;
-    lg_out[o] = s * (keep ? p.sa : 0.f);
-    z_out[o] = zred[c * BM + r] * p.sf;
-}
-
-// finish_scores for the fused pipeline: the thread's output item (row wave*16 + (lane & 15),
-// class lane >> 4) takes its row from registers (valid, sample counter tc, instance n, bag
-// counter cb) instead of the LDS row table. Same reductions, same arithmetic.
-template <int BM, int MAXC>
-__device__ __forceinline__ void score_rows(const GateParams& p, long long R0, float (&part)[MAXC][BM / 16],
-                                           f32x4 zacc, float* red, float* zred, int one_class,
-                                           int waves_per_gate, bool valid, uint32_t tc, uint32_t n,
-                                           uint32_t cb, float* lg_out, float* z_out, long long obase) {
-    constexpr int RT = BM / 16;
-    constexpr int NG = 4;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int ncls = one_class < 0 ? MAXC : 1;
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-        if (c >= ncls) break;
-        const int cls = one_class < 0 ? c : one_class;
-        if (cls >= MAXC) break;
-        float* dst = red + ((size_t)(wave * MAXC + cls) * NG + lane / 16) * BM + (lane % 16);
-#pragma unroll
-        for (int q = 0; q < RT; ++q) dst[16 * q] = part[c][q];
-    }
-    if (lane < 16) {
-#pragma unroll
-        for (int c = 0; c < MAXC; ++c) zred[c * BM + wave * 16 + lane] = zacc[c];
-    }
-    __syncthreads();
-    const int r = wave * 16 + (lane & 15), c = lane >> 4;
-    if (r >= BM || c >= p.C || !valid) return;
-    float s = 0.f;
-    const int nw = waves_per_gate ? waves_per_gate : kGateWaves;
-    for (int k = 0; k < nw; ++k) {
-        const int w = waves_per_gate ? c * waves_per_gate + k : k;
-        const float* src = red + (size_t)(w * MAXC + c) * NG * BM + r;
-#pragma unroll
-        for (int g = 0; g < NG; ++g) s += src[g * BM];
-    }
-    s += p.ba[c];
-    const bool keep = attention_keep(p.k0, p.k1, cb, tc, (uint32_t)c, n, p.thr_a);
     const size_t o = (size_t)(R0 + r - obase) * p.C + c;
     lg_out[o] = s * (keep ? p.sa : 0.f);
     z_out[o] = zred[c * BM + r] * p.sf;
@@ -679,7 +639,7 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
 #if MCGMIL_DIAG & 4   // ablation: no Philox (keep pattern from the counters)
             const uint4 o = make_uint4(cn * 0x9E3779B9u + (uint32_t)s, ct ^ cb, cn + ct, (uint32_t)s * 77u);
 #else
-            const uint4 o = philox4x32_10<true>((uint32_t)(s * 4 + kq), cn, ct, cb, p.k0, p.k1);
+            const uint4 o = philox4x32_10<true, MCGMIL_PHILOX_ROUNDS>((uint32_t)(s * 4 + kq), cn, ct, cb, p.k0, p.k1);
 #endif
             store_dropped(h, o, p.thrx_f, inval, slot + tid * 8);
         }
@@ -1019,7 +979,8 @@ __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GatePara
     // the region stay live across it, and the SGPR spills (into VGPR lanes) push the tile over
     // 256 VGPRs.
     Region* srg = reinterpret_cast<Region*>(sred + 32);
-    if (threadIdx.x == 0) *srg = rg;                 // read after the first tile's barrier
+    if (threadIdx.x == 0) *srg = rg;
+    __syncthreads();                                 // *srg is read by every wave from tile 0 on
     E* zw = reinterpret_cast<E*>(smem + fused_lds_bytes<E, MAXC>());
     if constexpr (fused_zl<E>())
         load_classifier_lds<E>(make_rsrc(p.Wp, p.wp_bytes), (uint32_t)(2 * p.P) * (uint32_t)(p.L >> 5) * 512u *

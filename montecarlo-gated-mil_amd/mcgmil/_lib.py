@@ -18,6 +18,11 @@ MCGMIL_BF16 = 1
 MCGMIL_U8 = 2
 MCGMIL_U16 = 3
 
+ABI_VERSION = 2
+# mcgmil_args.flags (include/mcgmil.h enum mcgmil_flags)
+PATH_FLAGS = {"auto": 0, "fused": 1, "two_kernel": 2}
+GATE_FLAGS = {"auto": 0, "pipe": 1 << 2, "pp": 2 << 2}
+
 EXPORTED = (
     "mcgmil_abi_version", "mcgmil_args_size", "mcgmil_last_error", "mcgmil_workspace_size",
     "mcgmil_packed_weights_size", "mcgmil_pack_weights", "mcgmil_mcdo_forward",
@@ -54,6 +59,7 @@ class Args(ctypes.Structure):
         ("keep_feat", _vp), ("keep_att", _vp),
         ("Y", _vp), ("A", _vp), ("A_mean", _vp), ("A_var", _vp), ("P_mean", _vp),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t), ("debug", _vp),
+        ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32),
     ]
 
 
@@ -167,6 +173,9 @@ def bind(path: str, mcdo_only: bool = False):
         f = getattr(L, name)
         f.argtypes = [pa, _vp, _vp]
         f.restype = ctypes.c_int
+    if L.mcgmil_abi_version() != ABI_VERSION:
+        raise MCGMILError(f"ABI mismatch: {path} has ABI version {L.mcgmil_abi_version()}, "
+                          f"the binding expects {ABI_VERSION}")
     if L.mcgmil_args_size() != ctypes.sizeof(Args):
         raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_args)={L.mcgmil_args_size()} but the "
                           f"ctypes mirror is {ctypes.sizeof(Args)} bytes")

@@ -109,7 +109,7 @@ def mc_predict_image(model, patcher, image: torch.Tensor, T: int = 100, seed: Op
     with ctx:
         H = model.extract_features(inst[None])      # NCHW: the stem kernel reads it as written
     _stage(events, "features", stream)
-    Y, A, st = model.mc_inference_features(H[0].float(), T=T, seed=seed, return_stats=True)
+    Y, A, st = model.mc_inference_features(H[0], T=T, seed=seed, return_stats=True)
     _stage(events, "mcdo_head", stream)
     probs = torch.softmax(Y[:, 0], dim=-1)                      # infer.py:195
     att_mean, att_std = patcher.attention_statistics(A, patcher.last_tile_ids, image.shape)

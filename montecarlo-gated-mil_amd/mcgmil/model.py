@@ -129,6 +129,19 @@ class MultiHeadGatedAttentionMIL(nn.Module):
             device = torch.device("cuda", torch.cuda.current_device())
         return device
 
+    def _offsets(self, n, bs, device):
+        """CSR offsets of bs bags of n instances, made on the device once per shape (infer.py:187-191
+        calls mc_inference once per bag: no per-call host->device copy or allocation)."""
+        key = (str(device), n, bs)
+        cache = self.__dict__.setdefault("_offs_cache", {})
+        t = cache.get(key)
+        if t is None:
+            if len(cache) > 64:
+                cache.clear()
+            t = cache[key] = ops.uniform_offsets(n, bs, device) if n > 0 else \
+                ops.bag_offsets_tensor([0] * bs, device)
+        return t
+
     # ------------------------------------------------------------------ kernel boundary
     def extract_features(self, x):
         """x [bs, n, 3, h, w] -> H [bs, n, L] (reference model.py:275-277)."""
@@ -151,7 +164,7 @@ class MultiHeadGatedAttentionMIL(nn.Module):
         pa = self.attention_dropouts[0].p if p_att is None else p_att
         head, packed = self.head_tensors(device)
         Hc = H.reshape(bs * n, L).to(self.compute_dtype).contiguous()
-        offs = ops.bag_offsets_tensor([n] * bs, device)
+        offs = self._offsets(n, bs, device)
         out = ops.mcdo_forward(Hc, offs, head, T, p_feat=pf, p_att=pa, seed=seed,
                                bag_id_base=bag_id_base, t_base=t_base, packed=packed,
                                return_attention=True, return_stats=return_stats)

@@ -76,9 +76,20 @@ class BagOffsets(torch.Tensor):
     uniform_rows: int = 0
 
 
+def uniform_offsets(n: int, bags: int, device) -> torch.Tensor:
+    """CSR offsets of `bags` bags of n instances each, made on the device (no host->device copy,
+    no synchronisation: the single-bag caller of infer.py:187-191 pays nothing for them)."""
+    if n < 1 or bags < 1 or n * bags >= 2**31:
+        raise ValueError("uniform bags need n >= 1, bags >= 1 and n * bags < 2^31")
+    t = torch.arange(0, n * (bags + 1), n, dtype=torch.int32, device=device).as_subclass(BagOffsets)
+    t.uniform_rows = n
+    return t
+
+
 def bag_offsets_tensor(sizes_or_offsets: Union[Sequence[int], torch.Tensor], device,
                        are_sizes: bool = True) -> torch.Tensor:
-    """Build the int32 CSR offsets [B+1] on `device` from bag sizes (or offsets)."""
+    """Build the int32 CSR offsets [B+1] on `device` from bag sizes (or offsets). The host copy
+    is pinned and copied asynchronously, so a caller with queued GPU work is not stalled."""
     x = torch.as_tensor(sizes_or_offsets, dtype=torch.int64).cpu()
     if are_sizes:
         x = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(x, 0)])
@@ -88,7 +99,10 @@ def bag_offsets_tensor(sizes_or_offsets: Union[Sequence[int], torch.Tensor], dev
         raise ValueError("total rows must fit int32")
     d = x[1:] - x[:-1]
     uniform = int(d[0]) if bool((d == d[0]).all()) and int(d[0]) > 0 else 0
-    t = x.to(device=device, dtype=torch.int32).as_subclass(BagOffsets)
+    x = x.to(torch.int32)
+    if torch.device(device).type == "cuda":
+        x = x.pin_memory()
+    t = x.to(device=device, non_blocking=True).as_subclass(BagOffsets)
     t.uniform_rows = uniform
     return t
 
@@ -97,9 +111,14 @@ def make_args(H: Optional[torch.Tensor], bag_offsets: torch.Tensor, head: Option
               T: int, C: int, G: int, D: int, p_feat: float, p_att: float, seed: int,
               bag_id_base: int = 0, t_base: int = 0, L: Optional[int] = None,
               total_rows: Optional[int] = None,
-              bag_ids: Optional[torch.Tensor] = None) -> _lib.Args:
-    """Fill struct mcgmil_args. With H=None, L and total_rows describe the (absent) features."""
+              bag_ids: Optional[torch.Tensor] = None, path: str = "auto",
+              gate: str = "auto") -> _lib.Args:
+    """Fill struct mcgmil_args. With H=None, L and total_rows describe the (absent) features.
+    path: "auto" | "fused" | "two_kernel", gate: "auto" | "pipe" | "pp" (mcgmil_args.flags)."""
+    if path not in _lib.PATH_FLAGS or gate not in _lib.GATE_FLAGS:
+        raise ValueError(f"path must be one of {list(_lib.PATH_FLAGS)}, gate one of {list(_lib.GATE_FLAGS)}")
     a = _lib.Args()
+    a.flags = _lib.PATH_FLAGS[path] | _lib.GATE_FLAGS[gate]
     a.L = H.shape[1] if H is not None else int(L)
     a.D = D
     a.C = C
@@ -162,12 +181,14 @@ def mcdo_forward(H: torch.Tensor, bag_offsets: torch.Tensor, head: HeadTensors, 
                  keep_feat: Optional[torch.Tensor] = None, keep_att: Optional[torch.Tensor] = None,
                  return_attention: bool = True, return_stats: bool = False,
                  packed: Optional[torch.Tensor] = None,
-                 bag_ids: Optional[torch.Tensor] = None) -> dict:
+                 bag_ids: Optional[torch.Tensor] = None, path: str = "auto",
+                 gate: str = "auto") -> dict:
     """All T MC-dropout samples of every bag in one call (mcgmil_mcdo_forward).
 
     H: [total_rows, L] fp32/bf16 on the GPU, bags as CSR row ranges bag_offsets[B+1] (int32,
     same device, last entry = total_rows). Bag b draws the Philox stream of bag counter
-    bag_ids[b] (int32 [B] on the device) if given, else bag_id_base + b. Returns a dict with
+    bag_ids[b] (int32 [B] on the device) if given, else bag_id_base + b. `path` / `gate` pick the
+    launch path (mcgmil_args.flags; every path gives bitwise the same outputs). Returns a dict with
       Y      [B, T, C]            class logits        (reference Y[T,1,C] per bag)
       A      [T*C*total_rows]     attention, per bag [T, C, N_b] (reference A[T,1,C,N])
       A_mean, A_var [C*total_rows], per bag [C, N_b];  P_mean [B, C]   (if return_stats)
@@ -179,7 +200,7 @@ def mcdo_forward(H: torch.Tensor, bag_offsets: torch.Tensor, head: HeadTensors, 
     if head.L != H.shape[1]:
         raise ValueError(f"H has L={H.shape[1]}, the head expects L={head.L}")
     a = make_args(H, bag_offsets, head, T, head.C, head.G, head.D, p_feat, p_att, seed,
-                  bag_id_base, t_base, bag_ids=bag_ids)
+                  bag_id_base, t_base, bag_ids=bag_ids, path=path, gate=gate)
     B, R, C = a.num_bags, a.total_rows, head.C
     if packed is not None:
         a.packed_w = _p(packed)

@@ -1,0 +1,47 @@
+#!/bin/bash
+# Round-4 GPU session: fused-kernel tests first, then the whole GPU suite, the config-5 bench and
+# the headline bench. Each step has its own limit; a fault/abort/timeout ends the script.
+set -u
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # name seconds cmd...
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name (limit ${secs}s)"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    grep -v "amdgpu.ids" "$OUT/$name.log" | tail -n 30
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "== stopping"; exit $rc; fi
+}
+for s in ${STEPS:-fusednew smoke fused all bench}; do
+    case $s in
+        fused) step pytest_fused 300 python -u -m pytest tests/test_gpu_fused.py -m gpu -x -q -rf --timeout 120 --timeout-method thread ;;
+        all) step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
+        cfg5) step bench_cfg5 600 python bench.py --workload cfg5 --steps 5 --warmup 2 --no-cpu-baseline ;;
+        bench) step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+        bench16) step bench16 600 python bench.py --bags 16 --no-cpu-baseline ;;
+        cfg4) step bench_cfg4 600 python3 bench.py --workload cfg4 --steps 10 --warmup 3 --no-cpu-baseline ;;
+        cfg4two) step bench_cfg4_twokernel 600 env MCGMIL_FUSED=0 python3 bench.py --workload cfg4 --steps 10 --warmup 3 --no-cpu-baseline ;;
+        benchtwo) step bench_twokernel 600 env MCGMIL_FUSED=0 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
+        abfused) step ab_fused 300 env MCGMIL_PROBE_LIBS="$(ls -1 abvar/*.so abvar2/*.so 2>/dev/null | paste -sd, -)" python -u scripts/probe_fused.py ;;
+        abfused128) step ab_fused128 300 env PROBE_N=128 MCGMIL_PROBE_LIBS="$(ls -1 abvar/*.so abvar2/*.so 2>/dev/null | paste -sd, -)" python -u scripts/probe_fused.py ;;
+        stamps) step stamps_flat 300 env PROBE_BAGS=128 python -u scripts/probe_stamps.py
+                step stamps_fused 300 env PROBE_BAGS=128 PROBE_FUSED=1 python -u scripts/probe_stamps.py ;;
+        listpmc) step list_pmc 120 rocprofv3 --list-avail ;;
+        drift) step probe_drift 600 env PROBE_CPU=1 python -u scripts/probe_cfg5_drift.py bf16 fp32 fp32nochunk fp32torch ;;
+        pmc) step pmc 1100 bash scripts/pmc_passes.sh ;;
+        pmcab) step pmc_ab 1200 env PROBE_ROUNDS=1 PMC_CMD="python3 scripts/probe_fused.py" bash scripts/pmc_passes.sh ;;
+        conv32) step pytest_conv32 600 python -u -m pytest tests/test_gpu_conv32.py tests/test_gpu_features.py tests/test_gpu_pipeline.py -m gpu -x -q -rf --timeout 300 --timeout-method thread ;;
+        probe32) step probe_conv32 600 python -u scripts/probe_conv32.py ;;
+        cfg5f32) step bench_cfg5_fp32 900 python bench.py --workload cfg5 --features fp32 --steps 3 --warmup 1 --no-cpu-baseline ;;
+        smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        fusednew) step pytest_fusednew 600 python -u -m pytest tests/test_gpu_fused.py -m gpu -x -v --timeout 300 --timeout-method thread -k "xcd or bench_step or path_flag" ;;
+        cfg4full) step pytest_cfg4full 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 400 --timeout-method thread -k "cfg4_full" ;;
+        single) step bench_single 300 python bench.py --workload single ;;
+        prof) rm -rf "$OUT/prof"; step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5
+              find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \; ;;
+    esac
+done
+echo "== done"

@@ -32,7 +32,8 @@ def test_gpus_flag_spawns_ranks(cuda):
     """`bench.py --gpus 2` with no launcher runs two ranks (here both on cuda:0 over gloo, the
     one-GPU rehearsal of the driver's multi-GPU run) and rank 0 reports n_gpus = 2."""
     r = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "2", "--same-device", "--dist-backend",
-                        "gloo", "--steps", "2", "--warmup", "1", "--bags", "4", "--no-cpu-baseline"],
+                        "gloo", "--steps", "2", "--warmup", "1", "--bags", "4", "--no-cpu-baseline",
+                        "--busy-seconds", "1"],
                        env=_env(), capture_output=True, text=True, timeout=600, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -42,7 +42,7 @@ def test_library_targets_gfx950(hip_lib):
 
 def test_args_struct_matches_binding(hip_lib):
     from mcgmil import _lib
-    assert hip_lib.mcgmil_abi_version() == 1
+    assert hip_lib.mcgmil_abi_version() == 2 == _lib.ABI_VERSION
     assert hip_lib.mcgmil_args_size() == ctypes.sizeof(_lib.Args)
     assert hip_lib.mcgmil_image_args_size() == ctypes.sizeof(_lib.ImageArgs)
     assert hip_lib.mcgmil_bn_args_size() == ctypes.sizeof(_lib.BnArgs)
@@ -82,11 +82,49 @@ def test_workspace_size_formula(hip_lib):
     ("L", 500, -2), ("L", 4096, -2), ("D", 100, -2), ("C", 5, -2), ("C", 0, -2), ("G", 3, -1),
     ("T", 0, -1), ("num_bags", 0, -1), ("p_feat", 1.5, -1), ("p_att", -0.1, -1),
     ("h_dtype", 7, -1), ("bag_offsets", None, -1), ("total_rows", -1, -1),
+    ("flags", 3, -1), ("flags", 3 << 2, -1), ("flags", 16, -1), ("reserved", 1, -1),
 ])
 def test_validation_errors(hip_lib, field, value, code):
     rc, _ = _ws(hip_lib, _args(**{field: value}))
     assert rc == code
     assert len(hip_lib.mcgmil_last_error()) > 0
+
+
+def _regions(hip_lib, a):
+    rc, n = _ws(hip_lib, a)
+    assert rc == 0
+    a.workspace, a.workspace_bytes = ctypes.c_void_p(0x100000), n
+    a.H, a.ldh = ctypes.c_void_p(0x3000), 512
+    a.bv = a.bu = a.wa = a.ba = ctypes.c_void_p(0x4000)
+    r = ctypes.c_int64(-1)
+    assert hip_lib.mcgmil_fused_regions(ctypes.byref(a), ctypes.byref(r)) == 0
+    return r.value
+
+
+def test_path_flags_select_the_launch(hip_lib, monkeypatch):
+    """mcgmil_args.flags picks the launch mcgmil_gate_softmax_pool makes (host logic, no launch):
+    auto = fused only for bf16 batches of equal-size bags with >= 16,384 regions; FUSED whenever
+    it applies; TWO_KERNEL never; MCGMIL_GATE_PP keeps bf16 heads off the fused (pipe) tile code;
+    MCGMIL_FUSED in the environment overrides the flags."""
+    from mcgmil import _lib
+    monkeypatch.delenv("MCGMIL_FUSED", raising=False)
+    F, G = _lib.PATH_FLAGS, _lib.GATE_FLAGS
+    small = dict(num_bags=16, total_rows=16 * 2048, uniform_bag_rows=2048)
+    big = dict(num_bags=512, total_rows=512 * 2048, uniform_bag_rows=2048)
+    assert _regions(hip_lib, _args(**small)) == 0
+    assert _regions(hip_lib, _args(**big)) == 512 * 50
+    assert _regions(hip_lib, _args(flags=F["fused"], **small)) == 16 * 50
+    assert _regions(hip_lib, _args(flags=F["two_kernel"], **big)) == 0
+    assert _regions(hip_lib, _args(flags=F["fused"] | G["pp"], **small)) == 0
+    assert _regions(hip_lib, _args(flags=F["fused"] | G["pipe"], **small)) == 16 * 50
+    assert _regions(hip_lib, _args(flags=F["fused"], h_dtype=_lib.MCGMIL_F32, **small)) == 16 * 50
+    assert _regions(hip_lib, _args(h_dtype=_lib.MCGMIL_F32, **big)) == 0      # fp32: auto stays off
+    monkeypatch.setenv("MCGMIL_FUSED", "1")
+    assert _regions(hip_lib, _args(flags=F["two_kernel"], **small)) == 16 * 50
+    monkeypatch.setenv("MCGMIL_FUSED", "0")
+    assert _regions(hip_lib, _args(flags=F["fused"], **big)) == 0
+    monkeypatch.setenv("MCGMIL_FUSED", "auto")
+    assert _regions(hip_lib, _args(flags=F["fused"], **small)) == 0
 
 
 def test_forward_rejects_missing_workspace(hip_lib):

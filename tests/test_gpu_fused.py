@@ -171,3 +171,119 @@ def test_fused_config3_bag_vs_oracle(cuda):
     np.testing.assert_allclose(out["Y"][0].cpu().numpy(), Yr, rtol=0, atol=1e-4)
     A = out["A"].cpu().numpy().reshape(T, 2, N)
     assert np.abs(A - Ar).max() / np.abs(Ar).max() <= 1e-4
+
+
+# ------------------------------------------------------------------ the launch bench.py times
+def _oracle_bag(H_rows, sd, T, seed, bag_ctr, N):
+    """Reference outputs (mcdo_ref, model.py:280-316) of one bag on its bf16 operands exactly:
+    H rows already bf16-representable, weights bf16-rounded; masks from the C Philox."""
+    kF, kA = mcdo_ref.masks_for_bag(seed, bag_ctr, T, N, 512, 2, 0.1, 0.1)
+    prm = mcdo_ref.HeadParams(synthetic.head_arrays(synthetic.round_state_dict_bf16(sd), 2, False))
+    Yr, Ar = mcdo_ref.mc_inference(H_rows, prm, kF, kA, 0.1, 0.1)
+    return Yr.numpy()[:, 0], Ar.numpy()[:, 0]                  # [T, C], [T, C, N]
+
+
+def _check_vs_oracle(out, b, sizes_before, N, T, Yr, Ar):
+    from test_gpu_parity import TOL_BF16_IN
+    Y = out["Y"][b].cpu().numpy()
+    o = T * 2 * sizes_before
+    A = out["A"][o:o + T * 2 * N].cpu().numpy().reshape(T, 2, N)
+    Am = out["A_mean"][2 * sizes_before:2 * sizes_before + 2 * N].cpu().numpy().reshape(2, N)
+    np.testing.assert_allclose(Y, Yr, rtol=0, atol=TOL_BF16_IN["Y"])
+    assert np.abs(A - Ar).max() / np.abs(Ar).max() <= TOL_BF16_IN["A"]
+    assert np.abs(Am - Ar.mean(0)).max() / np.abs(Ar.mean(0)).max() <= TOL_BF16_IN["A_mean"]
+
+
+@pytest.mark.parametrize("B", [8, 16])
+def test_fused_xcd_region_map_uniform_bags(cuda, B):
+    """The fused kernel's XCD region map (decode_region, mcgmil_kernels.h: uniform bags with
+    B % 8 == 0 -- the branch bench.py's 512-bag step runs): B bags of N = 256, T = 100, bf16
+    separate heads, per-bag global ids, forced fused through mcgmil_args.flags. Every output
+    bitwise equal to the two-kernel path; the first bag, the last and one on another XCD
+    (b % 8 == 5) against the reference restatement on the same bf16 operands."""
+    from mcgmil import ops
+    N, T, seed = 256, 100, 4242
+    sd = synthetic.head_state_dict(11, C=2, shared=False)
+    head = head_on(synthetic.head_arrays(sd, 2, False), cuda)
+    Hs = [synthetic.bf16_round(synthetic.bag_features(900 + b, N)) for b in range(B)]
+    H = torch.from_numpy(np.concatenate(Hs)).to(cuda).bfloat16()
+    offs = ops.bag_offsets_tensor([N] * B, cuda)
+    ids = [31 * b + 5 for b in range(B)]
+    kw = dict(p_feat=0.1, p_att=0.1, seed=seed, return_stats=True,
+              bag_ids=torch.tensor(ids, dtype=torch.int32, device=cuda))
+    assert offs.uniform_rows == N
+    assert regions(H, offs, head, T) == 0                       # auto: too few regions
+    a = ops.make_args(H, offs, head, T, 2, 2, 128, 0.1, 0.1, seed=1, path="fused")
+    import ctypes
+    from mcgmil import _lib
+    n = ctypes.c_size_t()
+    _lib.check(_lib.load().mcgmil_workspace_size(ctypes.byref(a), ctypes.byref(n)), "ws")
+    ws = torch.empty(n.value, dtype=torch.uint8, device=cuda)
+    a.workspace, a.workspace_bytes = ctypes.c_void_p(ws.data_ptr()), n.value
+    r = ctypes.c_int64()
+    _lib.check(_lib.load().mcgmil_fused_regions(ctypes.byref(a), ctypes.byref(r)), "fused_regions")
+    assert r.value == B * 7                                     # 16 t-groups per region: 7 per bag
+    out = ops.mcdo_forward(H, offs, head, T, path="fused", **kw)
+    ref = ops.mcdo_forward(H, offs, head, T, path="two_kernel", **kw)
+    again = ops.mcdo_forward(H, offs, head, T, path="fused", **kw)
+    torch.cuda.synchronize()
+    for k in ref:
+        assert torch.equal(out[k], ref[k]), k
+        assert torch.equal(out[k], again[k]), k
+    for b in sorted({0, 5, B - 1}):
+        Yr, Ar = _oracle_bag(Hs[b], sd, T, seed, ids[b], N)
+        _check_vs_oracle(out, b, b * N, N, T, Yr, Ar)
+
+
+def test_fused_bench_step_shape(cuda):
+    """bench.py's own step: 512 bags of N = 2048, T = 100, bf16 separate heads, default (auto)
+    policy = ONE gate_fused_kernel launch of 25,600 regions over the XCD region map. All outputs
+    bitwise equal to the two-kernel path and repeatable; bags 0, 13 (XCD 5) and 511 against the
+    reference restatement on the same bf16 operands (fp32 bounds x 10)."""
+    from mcgmil import ops
+    B, N, T, seed = 512, 2048, 100, 42
+    sd = synthetic.head_state_dict(0, C=2, shared=False)
+    head = head_on(synthetic.head_arrays(sd, 2, False), cuda)
+    g = torch.Generator(device=cuda).manual_seed(1000)
+    H = torch.randn(B * N, 512, device=cuda, generator=g).abs_().bfloat16()
+    offs = ops.bag_offsets_tensor([N] * B, cuda)
+    ids = torch.arange(B, dtype=torch.int32, device=cuda)
+    kw = dict(p_feat=0.1, p_att=0.1, seed=seed, bag_ids=ids, return_stats=True)
+    assert regions(H, offs, head, T) == B * 50
+    out = ops.mcdo_forward(H, offs, head, T, **kw)               # auto -> fused
+    ref = ops.mcdo_forward(H, offs, head, T, path="two_kernel", **kw)
+    torch.cuda.synchronize()
+    for k in ref:
+        assert torch.equal(out[k], ref[k]), k
+    del ref
+    again = ops.mcdo_forward(H, offs, head, T, **kw)
+    for k in out:
+        assert torch.equal(out[k], again[k]), k
+    del again
+    A = out["A"].view(B, T, 2, N)
+    assert torch.allclose(A.sum(-1), torch.ones(B, T, 2, device=cuda), atol=1e-5)
+    for b in (0, 13, 511):
+        Hb = H[b * N:(b + 1) * N].float().cpu().numpy()
+        Yr, Ar = _oracle_bag(Hb, sd, T, seed, b, N)
+        _check_vs_oracle(out, b, b * N, N, T, Yr, Ar)
+
+
+def test_path_flag_matches_environment_override(cuda):
+    """mcgmil_args.flags and the MCGMIL_FUSED override select the same launches (counted by
+    fused_regions) and give bitwise the same outputs."""
+    from mcgmil import ops
+    sizes = [300] * 8
+    sd = synthetic.head_state_dict(3, C=2, shared=False)
+    head = head_on(synthetic.head_arrays(sd, 2, False), cuda)
+    H = torch.from_numpy(np.concatenate([synthetic.bag_features(70 + b, n) for b, n in enumerate(sizes)])) \
+        .to(cuda).bfloat16()
+    offs = ops.bag_offsets_tensor(sizes, cuda)
+    kw = dict(p_feat=0.1, p_att=0.1, seed=9, return_stats=True)
+    a = ops.mcdo_forward(H, offs, head, 30, path="fused", **kw)
+    with fused("1"):
+        b = ops.mcdo_forward(H, offs, head, 30, path="two_kernel", **kw)   # env wins: fused
+    c = ops.mcdo_forward(H, offs, head, 30, path="two_kernel", gate="pipe", **kw)
+    for k in a:
+        assert torch.equal(a[k], b[k]) and torch.equal(a[k], c[k]), k
+    with pytest.raises(ValueError):
+        ops.mcdo_forward(H, offs, head, 30, path="bogus", **kw)

@@ -451,3 +451,57 @@ def test_cfg4_ragged_batch(cuda):
         np.testing.assert_allclose(Y[b], Yr[:, 0].numpy(), atol=TOL_BF16_IN["Y"])
         assert nrel(A[b].numpy().reshape(T, C, n), Ar[:, 0].numpy()) <= TOL_BF16_IN["A"]
         assert nrel(Am[b].numpy().reshape(C, n), Ar[:, 0].mean(0).numpy()) <= TOL_BF16_IN["A_mean"]
+
+
+def test_cfg4_full_size_one_launch(cuda):
+    """BASELINE config 4 at its stated size on one GPU: all 4,096 bags, N_b = rng(0).integers(256,
+    2049, 4096) (sum ~4.72 M instances), T = 100, bf16 separate heads, ONE varlen launch with the
+    global bag ids. Every bag: A sums to 1 over its instances for every (t, c), A_mean / A_var
+    equal the mean / unbiased variance of its A over T, P_mean the mean softmax of its Y; the whole
+    launch is bitwise repeatable; the smallest, the largest and two other bags against the
+    reference restatement on the same bf16 operands (fp32 bounds x 10)."""
+    from mcgmil import ops
+    sizes = np.random.default_rng(0).integers(256, 2049, 4096).tolist()
+    B, T, C, L, seed = len(sizes), 100, 2, 512, 42
+    R = int(sum(sizes))
+    sd = synthetic.head_state_dict(0, C=C, shared=False)
+    head = head_on(synthetic.head_arrays(sd, C, False), cuda)
+    g = torch.Generator(device=cuda).manual_seed(4)
+    H = torch.randn(R, L, device=cuda, generator=g).abs_().bfloat16()
+    offs = ops.bag_offsets_tensor(sizes, cuda)
+    ids = torch.arange(B, dtype=torch.int32, device=cuda)
+    kw = dict(p_feat=0.1, p_att=0.1, seed=seed, bag_ids=ids, return_stats=True)
+    out = ops.mcdo_forward(H, offs, head, T, **kw)
+    again = ops.mcdo_forward(H, offs, head, T, **kw)
+    for k in out:
+        assert torch.equal(out[k], again[k]), k
+    del again
+    n_t = torch.tensor(sizes, device=cuda, dtype=torch.int64)
+    # A: per bag [T, C, N_b] -> sums over instances, one per (bag, t, c)
+    sums = torch.segment_reduce(out["A"], "sum", lengths=n_t.repeat_interleave(T * C))
+    assert float((sums - 1).abs().max()) <= 1e-5
+    assert bool((out["A"] >= 0).all())
+    # A_mean / A_var against torch's mean / var over T, bag by bag on the device
+    err_m = torch.zeros((), device=cuda)
+    err_v = torch.zeros((), device=cuda)
+    Ab = torch.split(out["A"], (n_t * T * C).tolist())
+    Am = torch.split(out["A_mean"], (n_t * C).tolist())
+    Av = torch.split(out["A_var"], (n_t * C).tolist())
+    for b, n in enumerate(sizes):
+        a = Ab[b].view(T, C, n)
+        err_m = torch.maximum(err_m, (Am[b].view(C, n) - a.mean(0)).abs().max())
+        v = a.var(0)
+        err_v = torch.maximum(err_v, ((Av[b].view(C, n) - v).abs() - 1e-4 * v.abs()).max())
+    assert float(err_m) <= 1e-7 and float(err_v) <= 1e-12
+    P = torch.softmax(out["Y"], -1).mean(1)
+    assert torch.allclose(out["P_mean"], P, atol=1e-6)
+    prm = mcdo_ref.HeadParams(synthetic.head_arrays(synthetic.round_state_dict_bf16(sd), C, False))
+    starts = np.concatenate([[0], np.cumsum(sizes)])
+    for b in sorted({int(np.argmin(sizes)), int(np.argmax(sizes)), 1000, 4095}):
+        n = sizes[b]
+        Hb = H[starts[b]:starts[b + 1]].float().cpu().numpy()
+        kF, kA = mcdo_ref.masks_for_bag(seed, b, T, n, L, C, 0.1, 0.1)
+        Yr, Ar = mcdo_ref.mc_inference(Hb, prm, kF, kA, 0.1, 0.1)
+        np.testing.assert_allclose(out["Y"][b].cpu().numpy(), Yr[:, 0].numpy(), atol=TOL_BF16_IN["Y"])
+        assert nrel(Ab[b].cpu().numpy().reshape(T, C, n), Ar[:, 0].numpy()) <= TOL_BF16_IN["A"]
+        assert nrel(Am[b].cpu().numpy().reshape(C, n), Ar[:, 0].mean(0).numpy()) <= TOL_BF16_IN["A_mean"]
