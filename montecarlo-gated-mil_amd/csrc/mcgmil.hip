@@ -496,10 +496,13 @@ int mcgmil_bag_stats(const mcgmil_args* a, void* stream) {
     if (!a->Y) return fail(MCGMIL_E_INVALID, "Y is NULL");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const long long outs = (a->A_mean || a->A_var) ? a->total_rows * a->C : 0;
-    const int stat_blocks = (int)((outs + 255) / 256);
-    const int p_blocks = a->P_mean ? (a->num_bags * a->C + 255) / 256 : 0;
+    const long long sb = (outs + mcgmil::kStatOuts - 1) / mcgmil::kStatOuts;
+    if (sb > 0x7fffffffll) return fail(MCGMIL_E_UNSUPPORTED, "too many attention outputs for bag_stats_kernel");
+    const int stat_blocks = (int)sb;
+    constexpr int kBagsPerBlock = mcgmil::kStatThreads / mcgmil::kWave;   // P_mean: one wave per bag
+    const int p_blocks = a->P_mean ? (a->num_bags + kBagsPerBlock - 1) / kBagsPerBlock : 0;
     if (stat_blocks + p_blocks == 0) return MCGMIL_OK;
-    hipLaunchKernelGGL(mcgmil::bag_stats_kernel, dim3(stat_blocks + p_blocks), dim3(256), 0, s,
+    hipLaunchKernelGGL(mcgmil::bag_stats_kernel, dim3(stat_blocks + p_blocks), dim3(mcgmil::kStatThreads), 0, s,
                        a->bag_offsets, a->num_bags, a->T, a->C, (long long)a->total_rows,
                        stat_blocks, a->A, a->Y, a->A_mean, a->A_var, a->P_mean);
     hipError_t e = hipGetLastError();

@@ -1161,51 +1161,86 @@ __global__ __launch_bounds__(kGateThreads) void gate_scores_kernel(const GatePar
 
 // ---------------------------------------------------------------------------------------
 // bag_stats_kernel: mean and unbiased variance of the attention over the T passes
-// (infer.py:216-219: torch .mean/.std, var = std^2) -- one thread per output (bag, c, n),
-// coalesced over n -- and, in the trailing blocks, the mean class probability per (bag, c)
-// (infer.py:195 softmax over classes; net_utils.py:207-208 mean over T). Sums in fp64.
+// (infer.py:216-219: torch .mean/.std, var = std^2) per output (bag, c, n), and, in the trailing
+// blocks, the mean class probability per (bag, c) (infer.py:195 softmax over classes;
+// net_utils.py:207-208 mean over T). A 512-thread block takes 64 consecutive outputs (coalesced
+// over n) x 8 interleaved sample groups (t = g, g + 8, ...), so a lone bag of a few thousand
+// instances (the per-bag caller, infer.py:187-191) still spreads over dozens of CUs with ~T/8
+// loads per thread; the 8 group sums are added in group order (fp64, deterministic).
 // ---------------------------------------------------------------------------------------
+constexpr int kStatOuts = 64, kStatGroups = 8, kStatThreads = kStatOuts * kStatGroups;
 #ifndef MCGMIL_KERNELS_TEMPLATES_ONLY
-__global__ __launch_bounds__(256) void bag_stats_kernel(const int32_t* bag_off, int B, int T, int C,
-                                                        long long total_rows, int stat_blocks,
-                                                        const float* A, const float* Y,
-                                                        float* A_mean, float* A_var, float* P_mean) {
+__global__ __launch_bounds__(kStatThreads) void bag_stats_kernel(const int32_t* bag_off, int B, int T, int C,
+                                                                 long long total_rows, int stat_blocks,
+                                                                 const float* A, const float* Y,
+                                                                 float* A_mean, float* A_var, float* P_mean) {
     if ((int)blockIdx.x < stat_blocks) {
-        const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-        if (i >= total_rows * C) return;
-        const int bag = find_bag(bag_off, B, C, i);
-        const int ob = bag_off[bag];
-        const int Nb = bag_off[bag + 1] - ob;
-        const long long local = i - (long long)C * ob;
-        const int c = (int)(local / Nb);
-        const int n = (int)(local - (long long)c * Nb);
-        const float* a = A + (size_t)T * C * ob + (size_t)c * Nb + n;
-        const size_t step = (size_t)C * Nb;
+        __shared__ double ssum[kStatGroups][kStatOuts], ssq[kStatGroups][kStatOuts];
+        const int o = threadIdx.x % kStatOuts, grp = threadIdx.x / kStatOuts;
+        const long long i = (long long)blockIdx.x * kStatOuts + o;
+        const bool live = i < total_rows * C;
         double s = 0.0, ss = 0.0;
-#pragma unroll 10
-        for (int t = 0; t < T; ++t) {     // unrolled: the strided loads overlap (same sum order)
-            const double v = a[(size_t)t * step];
-            s += v;
-            ss += v * v;
+        if (live) {
+            const int bag = find_bag(bag_off, B, C, i);
+            const int ob = bag_off[bag];
+            const int Nb = bag_off[bag + 1] - ob;
+            const long long local = i - (long long)C * ob;
+            const int c = (int)(local / Nb);
+            const int n = (int)(local - (long long)c * Nb);
+            const float* a = A + (size_t)T * C * ob + (size_t)c * Nb + n;
+            const size_t step = (size_t)C * Nb;
+#pragma unroll 4
+            for (int t = grp; t < T; t += kStatGroups) {
+                const double v = a[(size_t)t * step];
+                s += v;
+                ss += v * v;
+            }
+        }
+        ssum[grp][o] = s;
+        ssq[grp][o] = ss;
+        __syncthreads();
+        if (grp != 0 || !live) return;
+        s = ssum[0][o];
+        ss = ssq[0][o];
+#pragma unroll
+        for (int g = 1; g < kStatGroups; ++g) {
+            s += ssum[g][o];
+            ss += ssq[g][o];
         }
         const double mean = s / T;
         if (A_mean) A_mean[i] = (float)mean;
         if (A_var) A_var[i] = T > 1 ? (float)fmax((ss - s * mean) / (T - 1), 0.0) : NAN;
         return;
     }
-    const int j = ((int)blockIdx.x - stat_blocks) * 256 + threadIdx.x;
-    if (!P_mean || j >= B * C) return;
-    const int b = j / C, c = j - b * C;
-    double acc = 0.0;
-    for (int t = 0; t < T; ++t) {
+    // P_mean: one wave per bag, lane l takes the samples t = l, l + 64, ... (the T samples' loads
+    // are independent: no serial latency chain over T), fp64 sums reduced over the wave in a
+    // fixed butterfly order
+    if (!P_mean) return;
+    const int b = ((int)blockIdx.x - stat_blocks) * (kStatThreads / kWave) + (int)(threadIdx.x / kWave);
+    const int lane = threadIdx.x % kWave;
+    if (b >= B) return;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int t = lane; t < T; t += kWave) {
         const float* y = Y + ((size_t)b * T + t) * C;
-        float m = y[0];
-        for (int k = 1; k < C; ++k) m = fmaxf(m, y[k]);
-        float sum = 0.f;
-        for (int k = 0; k < C; ++k) sum += expf(y[k] - m);
-        acc += (double)(expf(y[c] - m) / sum);
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = k < C ? y[k] : -INFINITY;
+        const float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+        float e[4], sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            e[k] = k < C ? expf(v[k] - m) : 0.f;
+            sum += e[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] += (double)(e[k] / sum);
     }
-    P_mean[j] = (float)(acc / T);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = wave_sum_d(acc[k]);
+    if (lane < C) {
+        const double a = lane == 0 ? acc[0] : lane == 1 ? acc[1] : lane == 2 ? acc[2] : acc[3];
+        P_mean[(size_t)b * C + lane] = (float)(a / T);
+    }
 }
 #endif
 

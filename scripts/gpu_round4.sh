@@ -20,6 +20,7 @@ for s in ${STEPS:-fusednew smoke fused all bench}; do
         fused) step pytest_fused 300 python -u -m pytest tests/test_gpu_fused.py -m gpu -x -q -rf --timeout 120 --timeout-method thread ;;
         all) step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
         cfg5) step bench_cfg5 600 python bench.py --workload cfg5 --steps 5 --warmup 2 --no-cpu-baseline ;;
+        parity) step pytest_parity 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fused.py -m gpu -x -q -rf --timeout 300 --timeout-method thread ;;
         bench) step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
         bench16) step bench16 600 python bench.py --bags 16 --no-cpu-baseline ;;
         cfg4) step bench_cfg4 600 python3 bench.py --workload cfg4 --steps 10 --warmup 3 --no-cpu-baseline ;;
@@ -40,6 +41,9 @@ for s in ${STEPS:-fusednew smoke fused all bench}; do
         fusednew) step pytest_fusednew 600 python -u -m pytest tests/test_gpu_fused.py -m gpu -x -v --timeout 300 --timeout-method thread -k "xcd or bench_step or path_flag" ;;
         cfg4full) step pytest_cfg4full 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 400 --timeout-method thread -k "cfg4_full" ;;
         single) step bench_single 300 python bench.py --workload single ;;
+        profsingle) rm -rf "$OUT/prof_single"; step rocprof_single 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_single" -o run --output-format csv -- python3 bench.py --workload single
+              find "$OUT/prof_single" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_single.csv" \; ;;
+        ab512) step ab_fused512 400 env PROBE_BAGS=512 MCGMIL_PROBE_LIBS="$(ls -1 abvar/*.so 2>/dev/null | paste -sd, -)" python -u scripts/probe_fused.py ;;
         prof) rm -rf "$OUT/prof"; step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5
               find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \; ;;
     esac
