@@ -585,11 +585,20 @@ constexpr int VPM = MCGMIL_VPM;   // VALU instructions scheduled after each MFMA
 #ifndef MCGMIL_SCHED
 #define MCGMIL_SCHED 0
 #endif
-constexpr int HD = 2;               // H prefetch distance of the pipelined kernel, in K steps
+#ifndef MCGMIL_HD
+#define MCGMIL_HD 2
+#endif
+constexpr int HD = MCGMIL_HD;       // H prefetch distance of the pipelined kernel, in K steps
+#ifndef MCGMIL_STAGGER
+#define MCGMIL_STAGGER 0            // 1: waves 4-7 run half a K step behind waves 0-3 (3 LDS slots)
+#endif
+// staging slots of the pipelined K loop (the staggered loop needs a third: see pipe_tile)
+template <typename E>
+__host__ __device__ constexpr int pipe_slots() { return MCGMIL_STAGGER && sizeof(E) == 2 ? 3 : 2; }
 
 template <typename E, int MAXC>
 __host__ __device__ constexpr size_t pipe_lds_bytes() {
-    return (size_t)2 * kPipeBM * 32 * sizeof(E) + (size_t)red_floats<kPipeBM, MAXC>() * 4 +
+    return (size_t)pipe_slots<E>() * kPipeBM * 32 * sizeof(E) + (size_t)red_floats<kPipeBM, MAXC>() * 4 +
            (size_t)MAXC * kPipeBM * 4 + (size_t)kRowInfo * kPipeBM * 4;
 }
 
@@ -736,42 +745,144 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
         __syncthreads();
     };
 
-    // prologue: stage step 0, load the weights of step 0 and H of step 1
-    Frag<E> wA[NJ], wB[NJ], zA, zB;
-    Raw<E> hA, hB;
-    hA = load_raw(hsrc);
-    hB = load_raw(hsrc + 32);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) wA[j] = wfrag(wsoff[j]);
-    if constexpr (ZL) {
-        // ZL: the classifier tile's fragments of all K steps sit in LDS (ZLOAD: loaded here, by
-        // this tile; else by the caller, once), so the K loop reads them with one ds_read per
-        // wave instead of 8 waves fetching the same 1 KiB per step. Visible after the barrier.
-        if constexpr (ZLOAD) load_classifier_lds<E>(wrs, zsoff, KS, zw);
-    } else {
-        zA = wfrag(zsoff);
-    }
-    stage(0, hA, Xs);
-    __syncthreads();
-    MCGMIL_STAMP(p, 2);
-
     // bf16 separate heads: the epilogue's head vectors load under the K loop instead of after it
     // (+0.3-1.4% in same-process A/B, bitwise equal; profiles/r02/gate_ab.log). The fp32 kernel
     // has no registers to spare for them.
     constexpr bool kEarlyHV = EARLY_HV && ONE_CLASS && sizeof(E) == 2;
     HeadVec hvec[PPW];
-    if constexpr (kEarlyHV) load_head_vectors<PPW>(p, q0, lane, hvec);
-    // KS is even and >= 2 (host guarantees L % 64 == 0). The first two steps are peeled: their
-    // MFMAs take the zero accumulators as an inline-constant C operand, so no register copies of
-    // the 132 zeroed accumulators are made on the way into the loop.
-    kstep(0, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA);
-    kstep(1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB);
+    // MCGMIL_STAGGER (timing studies): waves 4-7 run half a K step behind waves 0-3 -- between
+    // two barriers they finish the second half (weight fragments 2, 3) of step s-1 and start the
+    // first half (fragments 0, 1 + the classifier) of step s, so the two waves of a SIMD never
+    // reach the same phase of a step together. Legal with three staging slots: slot s % 3 is
+    // read up to the barrier after step s+1 and rewritten only with step s+3.
+    constexpr bool kStag = pipe_slots<E>() == 3 && NJ == 4;
+    if constexpr (kStag) {
+        if (wave >= 4) {
+            auto slot = [&](int s) { return Xs + (size_t)(s % 3) * SLOT; };
+            // interval s uses wh = w(s-1)[2,3] and wl = w(s)[0,1] and prefetches w(s)[2,3], w(s+1)[0,1]
+            auto lstep = [&](int s, bool second, const Frag<E> (&wh)[2], const Frag<E> (&wl)[2], const Frag<E>& z,
+                             Frag<E> (&whn)[2], Frag<E> (&wln)[2], Frag<E>& zn, const Raw<E>& h, Raw<E>& hn) {
+                const int s1 = s + 1 < KS ? s + 1 : KS - 1;
+                const int sh = s + HD < KS ? s + HD : KS - 1;
+                whn[0] = wfrag(wsoff[2] + (uint32_t)s * kStepBytes);
+                whn[1] = wfrag(wsoff[3] + (uint32_t)s * kStepBytes);
+                wln[0] = wfrag(wsoff[0] + (uint32_t)s1 * kStepBytes);
+                wln[1] = wfrag(wsoff[1] + (uint32_t)s1 * kStepBytes);
+                if constexpr (!ZL) zn = wfrag(zsoff + (uint32_t)s1 * kStepBytes);
+                hn = load_raw(hsrc + (size_t)sh * 32);
+                if (second) {      // (false only at s = 0, a literal at every call)
+                    const E* prv = slot(s + 2);
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt) {
+                        const Frag<E> x = load_frag(prv + (size_t)(rt * 64 + lane) * 8);
+                        acc[rt][2] = mma(wh[0], x, acc[rt][2]);
+                        acc[rt][3] = mma(wh[1], x, acc[rt][3]);
+                    }
+                }
+                const E* cur = slot(s);
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) {
+                    const Frag<E> x = load_frag(cur + (size_t)(rt * 64 + lane) * 8);
+                    acc[rt][0] = mma(wl[0], x, acc[rt][0]);
+                    acc[rt][1] = mma(wl[1], x, acc[rt][1]);
+                }
+                const Frag<E> xz = load_frag(cur + (size_t)tid * 8);
+                if constexpr (ZL) zacc = mma(load_frag(zw + (size_t)(s * 64 + lane) * 8), xz, zacc);
+                else zacc = mma(z, xz, zacc);
+                stage(s + 1, h, slot(s + 1));
+#pragma unroll
+                for (int i = 0; i < (second ? 2 * RT * 2 + 1 : RT * 2 + 1); ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0); // VALU
+                }
+                __syncthreads();
+            };
+            Frag<E> whA[2], wlA[2], whB[2], wlB[2], zA, zB;
+            Raw<E> hA, hB;
+            hA = load_raw(hsrc);
+            hB = load_raw(hsrc + 32);
+            wlA[0] = wfrag(wsoff[0]);
+            wlA[1] = wfrag(wsoff[1]);
+            if constexpr (ZL) {
+                if constexpr (ZLOAD) load_classifier_lds<E>(wrs, zsoff, KS, zw);
+            } else {
+                zA = wfrag(zsoff);
+            }
+            stage(0, hA, Xs);
+            __syncthreads();
+            MCGMIL_STAMP(p, 2);
+            if constexpr (kEarlyHV) load_head_vectors<PPW>(p, q0, lane, hvec);
+            lstep(0, false, whA, wlA, zA, whB, wlB, zB, hB, hA);
+            lstep(1, true, whB, wlB, zB, whA, wlA, zA, hA, hB);
+            for (int s = 2; s < KS; s += 2) {
+                lstep(s, true, whA, wlA, zA, whB, wlB, zB, hB, hA);
+                lstep(s + 1, true, whB, wlB, zB, whA, wlA, zA, hA, hB);
+            }
+            // the second half of the last step (its slot is not rewritten in this tile)
+            const E* prv = slot(KS - 1);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                const Frag<E> x = load_frag(prv + (size_t)(rt * 64 + lane) * 8);
+                acc[rt][2] = mma(whA[0], x, acc[rt][2]);
+                acc[rt][3] = mma(whA[1], x, acc[rt][3]);
+            }
+        } else {
+            auto slot = [&](int s) { return Xs + (size_t)(s % 3) * SLOT; };
+            Frag<E> wA[NJ], wB[NJ], zA, zB;
+            Raw<E> hA, hB;
+            hA = load_raw(hsrc);
+            hB = load_raw(hsrc + 32);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) wA[j] = wfrag(wsoff[j]);
+            if constexpr (ZL) {
+                if constexpr (ZLOAD) load_classifier_lds<E>(wrs, zsoff, KS, zw);
+            } else {
+                zA = wfrag(zsoff);
+            }
+            stage(0, hA, Xs);
+            __syncthreads();
+            MCGMIL_STAMP(p, 2);
+            if constexpr (kEarlyHV) load_head_vectors<PPW>(p, q0, lane, hvec);
+            kstep(0, slot(0), slot(1), wA, zA, wB, zB, hB, hA);
+            kstep(1, slot(1), slot(2), wB, zB, wA, zA, hA, hB);
+            for (int s = 2; s < KS; s += 2) {
+                kstep(s, slot(s), slot(s + 1), wA, zA, wB, zB, hB, hA);
+                kstep(s + 1, slot(s + 1), slot(s + 2), wB, zB, wA, zA, hA, hB);
+            }
+        }
+    } else {
+        // prologue: stage step 0, load the weights of step 0 and H of step 1
+        Frag<E> wA[NJ], wB[NJ], zA, zB;
+        Raw<E> hA, hB;
+        hA = load_raw(hsrc);
+        hB = load_raw(hsrc + 32);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) wA[j] = wfrag(wsoff[j]);
+        if constexpr (ZL) {
+            // ZL: the classifier tile's fragments of all K steps sit in LDS (ZLOAD: loaded here, by
+            // this tile; else by the caller, once), so the K loop reads them with one ds_read per
+            // wave instead of 8 waves fetching the same 1 KiB per step. Visible after the barrier.
+            if constexpr (ZLOAD) load_classifier_lds<E>(wrs, zsoff, KS, zw);
+        } else {
+            zA = wfrag(zsoff);
+        }
+        stage(0, hA, Xs);
+        __syncthreads();
+        MCGMIL_STAMP(p, 2);
+
+        if constexpr (kEarlyHV) load_head_vectors<PPW>(p, q0, lane, hvec);
+        // KS is even and >= 2 (host guarantees L % 64 == 0). The first two steps are peeled: their
+        // MFMAs take the zero accumulators as an inline-constant C operand, so no register copies of
+        // the 132 zeroed accumulators are made on the way into the loop.
+        kstep(0, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA);
+        kstep(1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB);
 #if MCGMIL_DIAG & 16   // ablation (timing only): 2 of the KS K steps
-    if (KS > 1000)
+        if (KS > 1000)
 #endif
-    for (int s = 2; s < KS; s += 2) {
-        kstep(s, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA);
-        kstep(s + 1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB);
+        for (int s = 2; s < KS; s += 2) {
+            kstep(s, Xs, Xs + SLOT, wA, zA, wB, zB, hB, hA);
+            kstep(s + 1, Xs + SLOT, Xs, wB, zB, wA, zA, hA, hB);
+        }
     }
     MCGMIL_STAMP(p, 3);
 
@@ -794,7 +905,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int BM = kPipeBM;
     E* Xs = reinterpret_cast<E*>(smem);                                   // [2][SLOT]
-    float* red = reinterpret_cast<float*>(smem + (size_t)2 * BM * 32 * sizeof(E));
+    float* red = reinterpret_cast<float*>(smem + (size_t)pipe_slots<E>() * BM * 32 * sizeof(E));
     float* zred = red + red_floats<BM, MAXC>();
     int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);
     const long long R0 = (long long)blockIdx.x * BM;
@@ -954,7 +1065,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GatePara
     constexpr int BM = kPipeBM;
     constexpr int CAP = fused_cap<MAXC>();
     E* Xs = reinterpret_cast<E*>(smem);                                   // [2][SLOT]
-    float* red = reinterpret_cast<float*>(smem + (size_t)2 * BM * 32 * sizeof(E));
+    float* red = reinterpret_cast<float*>(smem + (size_t)pipe_slots<E>() * BM * 32 * sizeof(E));
     float* zred = red + red_floats<BM, MAXC>();
     int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);               // [2][kRowInfo * BM]
     float* slg = reinterpret_cast<float*>(rinfo + 2 * kRowInfo * BM);    // [CAP][C]
