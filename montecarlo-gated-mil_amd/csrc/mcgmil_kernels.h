@@ -585,16 +585,12 @@ constexpr int VPM = MCGMIL_VPM;   // VALU instructions scheduled after each MFMA
 #ifndef MCGMIL_SCHED
 #define MCGMIL_SCHED 0
 #endif
-#ifndef MCGMIL_HD
-#define MCGMIL_HD 2
-#endif
-constexpr int HD = MCGMIL_HD;       // H prefetch distance of the pipelined kernel, in K steps
-#ifndef MCGMIL_STAGGER
-#define MCGMIL_STAGGER 0            // 1: waves 4-7 run half a K step behind waves 0-3 (3 LDS slots)
-#endif
-// staging slots of the pipelined K loop (the staggered loop needs a third: see pipe_tile)
+constexpr int HD = 2;               // H prefetch distance of the pipelined kernel, in K steps (the
+                                    // h / hn register rotation of the unrolled loop assumes 2)
+// staging slots of the pipelined K loop (a half-step stagger of waves 4-7 needed three; measured
+// 20% slower and removed, profiles/r04/gate_ab_r04.log run 2, code in commit 9d17683)
 template <typename E>
-__host__ __device__ constexpr int pipe_slots() { return MCGMIL_STAGGER && sizeof(E) == 2 ? 3 : 2; }
+__host__ __device__ constexpr int pipe_slots() { return 2; }
 
 template <typename E, int MAXC>
 __host__ __device__ constexpr size_t pipe_lds_bytes() {
@@ -750,107 +746,7 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
     // has no registers to spare for them.
     constexpr bool kEarlyHV = EARLY_HV && ONE_CLASS && sizeof(E) == 2;
     HeadVec hvec[PPW];
-    // MCGMIL_STAGGER (timing studies): waves 4-7 run half a K step behind waves 0-3 -- between
-    // two barriers they finish the second half (weight fragments 2, 3) of step s-1 and start the
-    // first half (fragments 0, 1 + the classifier) of step s, so the two waves of a SIMD never
-    // reach the same phase of a step together. Legal with three staging slots: slot s % 3 is
-    // read up to the barrier after step s+1 and rewritten only with step s+3.
-    constexpr bool kStag = pipe_slots<E>() == 3 && NJ == 4;
-    if constexpr (kStag) {
-        if (wave >= 4) {
-            auto slot = [&](int s) { return Xs + (size_t)(s % 3) * SLOT; };
-            // interval s uses wh = w(s-1)[2,3] and wl = w(s)[0,1] and prefetches w(s)[2,3], w(s+1)[0,1]
-            auto lstep = [&](int s, bool second, const Frag<E> (&wh)[2], const Frag<E> (&wl)[2], const Frag<E>& z,
-                             Frag<E> (&whn)[2], Frag<E> (&wln)[2], Frag<E>& zn, const Raw<E>& h, Raw<E>& hn) {
-                const int s1 = s + 1 < KS ? s + 1 : KS - 1;
-                const int sh = s + HD < KS ? s + HD : KS - 1;
-                whn[0] = wfrag(wsoff[2] + (uint32_t)s * kStepBytes);
-                whn[1] = wfrag(wsoff[3] + (uint32_t)s * kStepBytes);
-                wln[0] = wfrag(wsoff[0] + (uint32_t)s1 * kStepBytes);
-                wln[1] = wfrag(wsoff[1] + (uint32_t)s1 * kStepBytes);
-                if constexpr (!ZL) zn = wfrag(zsoff + (uint32_t)s1 * kStepBytes);
-                hn = load_raw(hsrc + (size_t)sh * 32);
-                if (second) {      // (false only at s = 0, a literal at every call)
-                    const E* prv = slot(s + 2);
-#pragma unroll
-                    for (int rt = 0; rt < RT; ++rt) {
-                        const Frag<E> x = load_frag(prv + (size_t)(rt * 64 + lane) * 8);
-                        acc[rt][2] = mma(wh[0], x, acc[rt][2]);
-                        acc[rt][3] = mma(wh[1], x, acc[rt][3]);
-                    }
-                }
-                const E* cur = slot(s);
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt) {
-                    const Frag<E> x = load_frag(cur + (size_t)(rt * 64 + lane) * 8);
-                    acc[rt][0] = mma(wl[0], x, acc[rt][0]);
-                    acc[rt][1] = mma(wl[1], x, acc[rt][1]);
-                }
-                const Frag<E> xz = load_frag(cur + (size_t)tid * 8);
-                if constexpr (ZL) zacc = mma(load_frag(zw + (size_t)(s * 64 + lane) * 8), xz, zacc);
-                else zacc = mma(z, xz, zacc);
-                stage(s + 1, h, slot(s + 1));
-#pragma unroll
-                for (int i = 0; i < (second ? 2 * RT * 2 + 1 : RT * 2 + 1); ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0); // VALU
-                }
-                __syncthreads();
-            };
-            Frag<E> whA[2], wlA[2], whB[2], wlB[2], zA, zB;
-            Raw<E> hA, hB;
-            hA = load_raw(hsrc);
-            hB = load_raw(hsrc + 32);
-            wlA[0] = wfrag(wsoff[0]);
-            wlA[1] = wfrag(wsoff[1]);
-            if constexpr (ZL) {
-                if constexpr (ZLOAD) load_classifier_lds<E>(wrs, zsoff, KS, zw);
-            } else {
-                zA = wfrag(zsoff);
-            }
-            stage(0, hA, Xs);
-            __syncthreads();
-            MCGMIL_STAMP(p, 2);
-            if constexpr (kEarlyHV) load_head_vectors<PPW>(p, q0, lane, hvec);
-            lstep(0, false, whA, wlA, zA, whB, wlB, zB, hB, hA);
-            lstep(1, true, whB, wlB, zB, whA, wlA, zA, hA, hB);
-            for (int s = 2; s < KS; s += 2) {
-                lstep(s, true, whA, wlA, zA, whB, wlB, zB, hB, hA);
-                lstep(s + 1, true, whB, wlB, zB, whA, wlA, zA, hA, hB);
-            }
-            // the second half of the last step (its slot is not rewritten in this tile)
-            const E* prv = slot(KS - 1);
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt) {
-                const Frag<E> x = load_frag(prv + (size_t)(rt * 64 + lane) * 8);
-                acc[rt][2] = mma(whA[0], x, acc[rt][2]);
-                acc[rt][3] = mma(whA[1], x, acc[rt][3]);
-            }
-        } else {
-            auto slot = [&](int s) { return Xs + (size_t)(s % 3) * SLOT; };
-            Frag<E> wA[NJ], wB[NJ], zA, zB;
-            Raw<E> hA, hB;
-            hA = load_raw(hsrc);
-            hB = load_raw(hsrc + 32);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) wA[j] = wfrag(wsoff[j]);
-            if constexpr (ZL) {
-                if constexpr (ZLOAD) load_classifier_lds<E>(wrs, zsoff, KS, zw);
-            } else {
-                zA = wfrag(zsoff);
-            }
-            stage(0, hA, Xs);
-            __syncthreads();
-            MCGMIL_STAMP(p, 2);
-            if constexpr (kEarlyHV) load_head_vectors<PPW>(p, q0, lane, hvec);
-            kstep(0, slot(0), slot(1), wA, zA, wB, zB, hB, hA);
-            kstep(1, slot(1), slot(2), wB, zB, wA, zA, hA, hB);
-            for (int s = 2; s < KS; s += 2) {
-                kstep(s, slot(s), slot(s + 1), wA, zA, wB, zB, hB, hA);
-                kstep(s + 1, slot(s + 1), slot(s + 2), wB, zB, wA, zA, hA, hB);
-            }
-        }
-    } else {
+    {
         // prologue: stage step 0, load the weights of step 0 and H of step 1
         Frag<E> wA[NJ], wB[NJ], zA, zB;
         Raw<E> hA, hB;
