@@ -287,3 +287,61 @@ def test_path_flag_matches_environment_override(cuda):
         assert torch.equal(a[k], b[k]) and torch.equal(a[k], c[k]), k
     with pytest.raises(ValueError):
         ops.mcdo_forward(H, offs, head, 30, path="bogus", **kw)
+
+
+def _random_cases(n=12, seed=2024):
+    rng = np.random.default_rng(seed)
+    cases = []
+    for i in range(n):
+        C = int(rng.choice([1, 2, 3, 4]))
+        shared = bool(rng.integers(0, 2)) if C > 1 else False
+        D = int(rng.choice([64, 128]))
+        B = int(rng.integers(1, 7))
+        sizes = [int(x) for x in rng.integers(0, 700, B)]
+        if rng.random() < 0.3:
+            sizes = [sizes[0]] * B                           # uniform: arithmetic region map
+        T = int(rng.integers(1, 41))
+        p_f = float(rng.choice([0.0, 0.1, 0.37, 1.0]))
+        p_a = float(rng.choice([0.0, 0.1, 0.5, 1.0]))
+        dtype = torch.bfloat16 if rng.random() < 0.5 else torch.float32
+        cases.append((f"r{i}", dtype, sizes, T, C, shared, D, p_f, p_a))
+    return cases
+
+
+@pytest.mark.parametrize("case", _random_cases(), ids=lambda c: c[0])
+def test_random_shapes_fused_two_kernel_oracle(cuda, case):
+    """Seeded random sweep over the fused launch's parameter space (bag sizes incl. 0, T, C, head
+    layout, D, dropout p incl. 0 and 1, dtype): the fused and two-kernel paths bitwise equal, and
+    every non-empty bag against the reference restatement (mcdo_ref, model.py:280-316) with the
+    kernel's own masks, on the same operands (bf16-rounded for bf16) at the fp32 bounds (x 10)."""
+    from mcgmil import ops
+    from test_gpu_parity import TOL32, TOL_BF16_IN
+    name, dtype, sizes, T, C, shared, D, p_f, p_a = case
+    L, seed = 512, 4000 + int(name[1:])
+    sd = synthetic.head_state_dict(seed, L=L, D=D, C=C, shared=shared)
+    bf16 = dtype == torch.bfloat16
+    Hs = [synthetic.bag_features(seed + 10 + b, n, L) for b, n in enumerate(sizes)]
+    if bf16:
+        Hs = [synthetic.bf16_round(h) for h in Hs]
+    head = head_on(synthetic.head_arrays(sd, C, shared), cuda)
+    H = torch.from_numpy(np.concatenate(Hs)).to(cuda).to(dtype).contiguous()
+    offs = ops.bag_offsets_tensor(sizes, cuda)
+    kw = dict(p_feat=p_f, p_att=p_a, seed=seed, bag_id_base=17, return_stats=True)
+    two = ops.mcdo_forward(H, offs, head, T, path="two_kernel", **kw)
+    fz = ops.mcdo_forward(H, offs, head, T, path="fused", **kw)
+    for k in two:
+        assert torch.equal(torch.nan_to_num(fz[k], nan=7.0), torch.nan_to_num(two[k], nan=7.0)), k
+    tol = TOL_BF16_IN if bf16 else TOL32
+    sd_ref = synthetic.round_state_dict_bf16(sd) if bf16 else sd
+    prm = mcdo_ref.HeadParams(synthetic.head_arrays(sd_ref, C, shared))
+    Y = two["Y"].cpu().numpy()
+    A = ops.split_bags(two["A"].cpu(), sizes, T * C)
+    for b, n in enumerate(sizes):
+        if n == 0:
+            assert np.all(Y[b] == 0)
+            continue
+        kF, kA = mcdo_ref.masks_for_bag(seed, 17 + b, T, n, L, C, p_f, p_a)
+        Yr, Ar = mcdo_ref.mc_inference(Hs[b], prm, kF, kA, p_f, p_a)
+        np.testing.assert_allclose(Y[b], Yr[:, 0].numpy(), rtol=0, atol=tol["Y"])
+        Ar = Ar[:, 0].numpy()
+        assert np.abs(A[b].numpy().reshape(T, C, n) - Ar).max() <= tol["A"] * max(np.abs(Ar).max(), 1e-30)
