@@ -353,12 +353,17 @@ __device__ __forceinline__ void softmax_group(int ltid, bool active, int Nb, int
         // order are the register path's below, so A and Y are bitwise the same.
         float (*sred2)[4] = reinterpret_cast<float (*)[4]>(sred);
         float e0[kSoftmaxRows], e1[kSoftmaxRows];
+        float2 zr[kSoftmaxRows];          // z loaded with the logits: one memory round trip, not two
         float m0 = -INFINITY, m1 = -INFINITY;
 #pragma unroll
         for (int k = 0; k < kSoftmaxRows; ++k) {
             const int n = tid + 256 * k;
             float2 l = make_float2(-INFINITY, -INFINITY);
-            if (n < Nl) l = *reinterpret_cast<const float2*>(lg + (size_t)n * 2);
+            zr[k] = make_float2(0.f, 0.f);
+            if (n < Nl) {
+                l = *reinterpret_cast<const float2*>(lg + (size_t)n * 2);
+                zr[k] = *reinterpret_cast<const float2*>(zz + (size_t)n * 2);
+            }
             e0[k] = l.x;
             e1[k] = l.y;
             m0 = fmaxf(m0, e0[k]);
@@ -376,7 +381,7 @@ __device__ __forceinline__ void softmax_group(int ltid, bool active, int Nb, int
         for (int k = 0; k < kSoftmaxRows; ++k) {
             const int n = tid + 256 * k;
             if (n < Nl) {
-                const float2 z = *reinterpret_cast<const float2*>(zz + (size_t)n * 2);
+                const float2 z = zr[k];
                 e0[k] = expf(e0[k] - m0);
                 e1[k] = expf(e1[k] - m1);
                 s0 += e0[k];
@@ -1196,11 +1201,22 @@ __global__ __launch_bounds__(kStatThreads) void bag_stats_kernel(const int32_t* 
             const int n = (int)(local - (long long)c * Nb);
             const float* a = A + (size_t)T * C * ob + (size_t)c * Nb + n;
             const size_t step = (size_t)C * Nb;
-#pragma unroll 4
-            for (int t = grp; t < T; t += kStatGroups) {
-                const double v = a[(size_t)t * step];
-                s += v;
-                ss += v * v;
+            // chunks of 16 samples per thread: all 16 loads in flight before the (in-order) sums
+            for (int t0 = grp; t0 < T; t0 += 16 * kStatGroups) {
+                float v[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const int t = t0 + k * kStatGroups;
+                    v[k] = t < T ? a[(size_t)t * step] : 0.f;
+                }
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    if (t0 + k * kStatGroups < T) {
+                        const double d = v[k];
+                        s += d;
+                        ss += d * d;
+                    }
+                }
             }
         }
         ssum[grp][o] = s;
