@@ -1201,22 +1201,11 @@ __global__ __launch_bounds__(kStatThreads) void bag_stats_kernel(const int32_t* 
             const int n = (int)(local - (long long)c * Nb);
             const float* a = A + (size_t)T * C * ob + (size_t)c * Nb + n;
             const size_t step = (size_t)C * Nb;
-            // chunks of 16 samples per thread: all 16 loads in flight before the (in-order) sums
-            for (int t0 = grp; t0 < T; t0 += 16 * kStatGroups) {
-                float v[16];
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const int t = t0 + k * kStatGroups;
-                    v[k] = t < T ? a[(size_t)t * step] : 0.f;
-                }
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    if (t0 + k * kStatGroups < T) {
-                        const double d = v[k];
-                        s += d;
-                        ss += d * d;
-                    }
-                }
+#pragma unroll 4
+            for (int t = grp; t < T; t += kStatGroups) {
+                const double v = a[(size_t)t * step];
+                s += v;
+                ss += v * v;
             }
         }
         ssum[grp][o] = s;
