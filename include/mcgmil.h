@@ -47,7 +47,8 @@
 extern "C" {
 #endif
 
-#define MCGMIL_ABI_VERSION 2   /* 2: mcgmil_args.flags (path selection) */
+#define MCGMIL_ABI_VERSION 3   /* 2: mcgmil_args.flags (path selection); 3: mcgmil_conv_args.flags,
+                                  mcgmil_stem_args.flags (mcgmil_features.h) */
 
 enum mcgmil_status {
     MCGMIL_OK = 0,

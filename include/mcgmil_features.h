@@ -115,7 +115,19 @@ typedef struct mcgmil_conv_args {
                                    writing and re-reading bn(x). Only where
                                    mcgmil_conv_input_bn() reports support (the 3x3 / stride 1 halo
                                    kernels), else MCGMIL_E_UNSUPPORTED. NULL: x as is */
+    int32_t flags;              /* mcgmil_conv_flags: the kernel shape (0 = auto; performance only,
+                                   every shape computes the same sums; MCGMIL_CONV_TILE in the
+                                   environment -- nohalo | small | big512 -- overrides) */
+    int32_t reserved;           /* must be 0 */
 } mcgmil_conv_args;
+
+/* mcgmil_conv_args.flags */
+enum mcgmil_conv_flags {
+    MCGMIL_CONV_TILE_AUTO = 0,     /* the measured-fastest kernel per layer shape */
+    MCGMIL_CONV_TILE_NOHALO = 1,   /* no halo-patch kernels (generic LDS-DMA kernel everywhere) */
+    MCGMIL_CONV_TILE_SMALL = 2,    /* 256 x 128 tiles where auto would take 256 x 256 */
+    MCGMIL_CONV_TILE_BIG512 = 3    /* 512 x 128 tiles on 128-channel layers */
+};
 
 size_t mcgmil_conv_args_size(void);
 int mcgmil_pack_conv_weights(const mcgmil_conv_args* a, const void* weight, int32_t weight_dtype,
@@ -151,7 +163,17 @@ typedef struct mcgmil_stem_args {
     float* batch_invstd;        /* optional out [64] */
     void* workspace;            /* >= mcgmil_stem_workspace_size() bytes, 256-byte aligned */
     size_t workspace_bytes;
+    int32_t flags;              /* mcgmil_stem_flags (0 = auto; performance only, same results;
+                                   MCGMIL_STEM_HPOOL=0 in the environment overrides) */
+    int32_t reserved;           /* must be 0 */
 } mcgmil_stem_args;
+
+/* mcgmil_stem_args.flags */
+enum mcgmil_stem_flags {
+    MCGMIL_STEM_AUTO = 0,            /* the 3x3/2 max-pool split: horizontal half in the convolution
+                                        epilogue, vertical half in the BatchNorm pass */
+    MCGMIL_STEM_POOL_UNSPLIT = 1     /* the convolution writes the whole activation; one pooling pass */
+};
 
 size_t mcgmil_stem_args_size(void);
 int mcgmil_stem_packed_size(const mcgmil_stem_args* a, size_t* bytes);

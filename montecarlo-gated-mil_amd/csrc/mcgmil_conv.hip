@@ -890,12 +890,21 @@ ConvGeom geom_of(const mcgmil_conv_args* a) {
     return g;
 }
 
-// MCGMIL_CONV_TILE=nohalo keeps layer-1 shapes on the generic kernel (A/B timing)
-Plan make_plan(ConvGeom& g) {
+// The tile policy: args->flags (mcgmil_conv_flags), or MCGMIL_CONV_TILE=nohalo|small|big512 in the
+// environment, which overrides the flags (A/B timing of an unmodified caller)
+int tile_policy(int flags) {
+    const char* e = getenv("MCGMIL_CONV_TILE");
+    if (e && !strcmp(e, "nohalo")) return MCGMIL_CONV_TILE_NOHALO;
+    if (e && !strcmp(e, "small")) return MCGMIL_CONV_TILE_SMALL;
+    if (e && !strcmp(e, "big512")) return MCGMIL_CONV_TILE_BIG512;
+    return flags;
+}
+
+Plan make_plan(ConvGeom& g, int flags) {
     Plan p;
     const int cus = cu_count();
-    const char* force = getenv("MCGMIL_CONV_TILE");
-    const bool halo_ok = !(force && !strcmp(force, "nohalo"));
+    const int policy = tile_policy(flags);
+    const bool halo_ok = policy != MCGMIL_CONV_TILE_NOHALO;
     if (halo_ok && g.Cin == 64 && g.Cout == 64 && g.KH == 3 && g.KW == 3 && g.stride == 1 && g.pad == 1) {
         HaloGeom hg;
         hg.WP = g.W + 2;
@@ -951,9 +960,9 @@ Plan make_plan(ConvGeom& g) {
     // 128 x 64 wave tiles (25% less LDS fragment traffic per MFMA than 64 x 64), two LDS stages:
     // 256 x 256 when Cout % 256 == 0 (layer 3: +30-34%, layer 4: +7%, measured in one process);
     // 512 x 128 measured slower on the 128-channel layer (kept for MCGMIL_CONV_TILE=big512);
-    // MCGMIL_CONV_TILE=small keeps 256 x 128
-    const bool small = force && !strcmp(force, "small");
-    const bool big512 = force && !strcmp(force, "big512");
+    // MCGMIL_CONV_TILE_SMALL keeps 256 x 128
+    const bool small = policy == MCGMIL_CONV_TILE_SMALL;
+    const bool big512 = policy == MCGMIL_CONV_TILE_BIG512;
     if (!small && BN == 128 && (g.Cout % 256 == 0 || big512)) {
         const int bm = g.Cout % 256 == 0 ? 256 : 512, bn = g.Cout % 256 == 0 ? 256 : 128;
         g.tiles_m = (g.M + bm - 1) / bm;
@@ -1035,6 +1044,8 @@ int validate(const mcgmil_conv_args* a) {
         return fail(MCGMIL_E_UNSUPPORTED, "kernel size must be in 1..7");
     if (a->stride < 1 || a->pad < 0) return fail(MCGMIL_E_INVALID, "stride must be >= 1 and pad >= 0");
     if (a->in_relu != 0 && a->in_relu != 1) return fail(MCGMIL_E_INVALID, "in_relu must be 0 or 1");
+    if (a->flags < MCGMIL_CONV_TILE_AUTO || a->flags > MCGMIL_CONV_TILE_BIG512 || a->reserved != 0)
+        return fail(MCGMIL_E_INVALID, "flags must be an mcgmil_conv_flags value and reserved 0");
     if (a->height > 16383 || a->width > 16383 || a->pad > 64)
         return fail(MCGMIL_E_UNSUPPORTED, "height and width must be <= 16383 and pad <= 64");
     const long long oh = ((long long)a->height + 2 * a->pad - a->kernel_h) / a->stride + 1;
@@ -1083,7 +1094,7 @@ int mcgmil_conv_input_bn(const mcgmil_conv_args* a, int32_t* supported) {
     mcgmil_conv_args b = *a;
     b.in_ab = reinterpret_cast<const float*>(16);   // a plan with the input BatchNorm
     ConvGeom g = geom_of(&b);
-    const int kind = make_plan(g).kind;
+    const int kind = make_plan(g, a->flags).kind;
     *supported = kind == 1 || kind == 4;
     return MCGMIL_OK;
 }
@@ -1093,7 +1104,7 @@ int mcgmil_conv_stats_parts(const mcgmil_conv_args* a, int32_t* parts) {
     if (rc) return rc;
     if (!parts) return fail(MCGMIL_E_INVALID, "parts is NULL");
     ConvGeom g = geom_of(a);
-    *parts = make_plan(g).parts;
+    *parts = make_plan(g, a->flags).parts;
     return MCGMIL_OK;
 }
 
@@ -1106,7 +1117,7 @@ int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream) {
     if ((uintptr_t)a->stats & 3u) return fail(MCGMIL_E_ALIGN, "stats must be 4-byte aligned");
     if ((uintptr_t)a->in_ab & 3u) return fail(MCGMIL_E_ALIGN, "in_ab must be 4-byte aligned");
     ConvGeom g = geom_of(a);
-    const Plan p = make_plan(g);
+    const Plan p = make_plan(g, a->flags);
     if (a->in_ab && p.kind != 1 && p.kind != 4)
         return fail(MCGMIL_E_UNSUPPORTED, "in_ab: this layer's kernel has no input BatchNorm "
                                           "(see mcgmil_conv_input_bn)");

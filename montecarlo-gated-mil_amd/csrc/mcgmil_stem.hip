@@ -88,6 +88,8 @@ int geometry(const mcgmil_stem_args* a, Geometry* out) {
         return fail(MCGMIL_E_UNSUPPORTED, "the stem kernel needs stride 2 and kernel + (pad & 1) <= 8");
     if (a->width & 1) return fail(MCGMIL_E_UNSUPPORTED, "the stem kernel needs an even width");
     if (a->relu != 0 && a->relu != 1) return fail(MCGMIL_E_INVALID, "relu must be 0 or 1");
+    if ((a->flags != MCGMIL_STEM_AUTO && a->flags != MCGMIL_STEM_POOL_UNSPLIT) || a->reserved != 0)
+        return fail(MCGMIL_E_INVALID, "flags must be an mcgmil_stem_flags value and reserved 0");
     const int OH = (a->height + 2 * a->pad - a->kernel) / 2 + 1;
     const int OW = (a->width + 2 * a->pad - a->kernel) / 2 + 1;
     if (a->height + 2 * a->pad < a->kernel || a->width + 2 * a->pad < a->kernel || OH < 1 || OW < 1)
@@ -492,9 +494,10 @@ int mcgmil_stem_forward(const mcgmil_stem_args* a, void* stream) {
     g.part = reinterpret_cast<float*>(ws + c.part);
     g.gamma = a->gamma;
     // the ResNet pool (3 x 3, stride 2, pad 1) on an even width: horizontal half in the epilogue
+    // args->flags MCGMIL_STEM_POOL_UNSPLIT, or MCGMIL_STEM_HPOOL=0 in the environment (overrides)
     const char* hp_env = getenv("MCGMIL_STEM_HPOOL");
-    const bool hp = a->pool_kernel == 3 && a->pool_stride == 2 && a->pool_pad == 1 && G.OW % 2 == 0 &&
-                    !(hp_env && !strcmp(hp_env, "0"));
+    const bool unsplit = hp_env ? !strcmp(hp_env, "0") : a->flags == MCGMIL_STEM_POOL_UNSPLIT;
+    const bool hp = a->pool_kernel == 3 && a->pool_stride == 2 && a->pool_pad == 1 && G.OW % 2 == 0 && !unsplit;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(stem_prep_kernel, dim3(1), dim3(256), 0, s, g, G.KS, (int)stats);
     switch (G.KS) {

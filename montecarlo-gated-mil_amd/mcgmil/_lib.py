@@ -18,7 +18,7 @@ MCGMIL_BF16 = 1
 MCGMIL_U8 = 2
 MCGMIL_U16 = 3
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 # mcgmil_args.flags (include/mcgmil.h enum mcgmil_flags)
 PATH_FLAGS = {"auto": 0, "fused": 1, "two_kernel": 2}
 GATE_FLAGS = {"auto": 0, "pipe": 1 << 2, "pp": 2 << 2}
@@ -91,6 +91,7 @@ class ConvArgs(ctypes.Structure):
         ("kernel_h", ctypes.c_int32), ("kernel_w", ctypes.c_int32), ("stride", ctypes.c_int32),
         ("pad", ctypes.c_int32), ("in_relu", ctypes.c_int32),
         ("x", _vp), ("w", _vp), ("y", _vp), ("stats", _vp), ("in_ab", _vp),
+        ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32),
     ]
 
 
@@ -105,6 +106,7 @@ class StemArgs(ctypes.Structure):
         ("running_mean", _vp), ("running_var", _vp), ("y", _vp),
         ("batch_mean", _vp), ("batch_invstd", _vp),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
+        ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32),
     ]
 
 

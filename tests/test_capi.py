@@ -42,7 +42,9 @@ def test_library_targets_gfx950(hip_lib):
 
 def test_args_struct_matches_binding(hip_lib):
     from mcgmil import _lib
-    assert hip_lib.mcgmil_abi_version() == 2 == _lib.ABI_VERSION
+    assert hip_lib.mcgmil_abi_version() == 3 == _lib.ABI_VERSION
+    assert hip_lib.mcgmil_conv_args_size() == ctypes.sizeof(_lib.ConvArgs)
+    assert hip_lib.mcgmil_stem_args_size() == ctypes.sizeof(_lib.StemArgs)
     assert hip_lib.mcgmil_args_size() == ctypes.sizeof(_lib.Args)
     assert hip_lib.mcgmil_image_args_size() == ctypes.sizeof(_lib.ImageArgs)
     assert hip_lib.mcgmil_bn_args_size() == ctypes.sizeof(_lib.BnArgs)
@@ -202,6 +204,9 @@ def test_stem_sizes_and_validation(hip_lib):
         a = _stem(width=1000) if k == "width_wide" else _stem(**{k: v})
         assert hip_lib.mcgmil_stem_workspace_size(ctypes.byref(a), ctypes.byref(n)) == -2, k
     assert hip_lib.mcgmil_stem_workspace_size(ctypes.byref(_stem(relu=3)), ctypes.byref(n)) == -1
+    assert hip_lib.mcgmil_stem_workspace_size(ctypes.byref(_stem(flags=1)), ctypes.byref(n)) == 0
+    assert hip_lib.mcgmil_stem_workspace_size(ctypes.byref(_stem(flags=2)), ctypes.byref(n)) == -1
+    assert hip_lib.mcgmil_stem_workspace_size(ctypes.byref(_stem(reserved=1)), ctypes.byref(n)) == -1
     assert hip_lib.mcgmil_stem_forward(ctypes.byref(_stem()), None) == -1   # NULL x / w / y
 
 
@@ -235,6 +240,14 @@ def test_conv_stats_parts_and_validation(hip_lib):
         assert hip_lib.mcgmil_conv_input_bn(ctypes.byref(args), ctypes.byref(p)) == 0
         assert p.value == want, (args.in_channels, args.width, p.value)
     assert hip_lib.mcgmil_conv_input_bn(ctypes.byref(conv(64, 64, 3, 1, 1, in_relu=2)), ctypes.byref(p)) == -1
+    # flags (mcgmil_conv_flags): NOHALO keeps layer 1 off the halo kernel (no input BN there),
+    # SMALL gives the 256-channel layer statistics rows again (256 x 128 tiles); bad values refused
+    assert hip_lib.mcgmil_conv_input_bn(ctypes.byref(conv(64, 64, 3, 1, 1, 56, flags=1)), ctypes.byref(p)) == 0
+    assert p.value == 0
+    assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(256, 256, 3, 1, 1, 14, flags=2)), ctypes.byref(p)) == 0
+    assert p.value >= 1
+    assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 64, 3, 1, 1, flags=4)), ctypes.byref(p)) == -1
+    assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 64, 3, 1, 1, reserved=1)), ctypes.byref(p)) == -1
 
 
 def test_batchnorm_coefficients_validation(hip_lib):
