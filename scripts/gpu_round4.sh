@@ -34,7 +34,7 @@ for s in ${STEPS:-fusednew smoke fused all bench}; do
                 step stamps_fused 300 env PROBE_BAGS=128 PROBE_FUSED=1 python -u scripts/probe_stamps.py ;;
         listpmc) step list_pmc 120 rocprofv3 --list-avail ;;
         drift) step probe_drift 600 env PROBE_CPU=1 python -u scripts/probe_cfg5_drift.py bf16 fp32 fp32nochunk fp32torch ;;
-        pmc) step pmc 1100 bash scripts/pmc_passes.sh ;;
+        pmc) step pmc 1100 env PMC_CMD="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --busy-seconds 0 --no-secondary" PASSES="fetch write sq coex" bash scripts/pmc_passes.sh ;;
         pmcab) step pmc_ab 1200 env PROBE_ROUNDS=1 PMC_CMD="python3 scripts/probe_fused.py" bash scripts/pmc_passes.sh ;;
         conv32) step pytest_conv32 600 python -u -m pytest tests/test_gpu_conv32.py tests/test_gpu_features.py tests/test_gpu_pipeline.py -m gpu -x -q -rf --timeout 300 --timeout-method thread ;;
         probe32) step probe_conv32 600 python -u scripts/probe_conv32.py ;;
