@@ -14,7 +14,6 @@
 #include "mcgmil_kernels.h"
 #include "mcgmil_gate_pp.h"
 #include "mcgmil_fused.h"
-#include "mcgmil_gate_w4.h"
 
 namespace mcgmil_detail {
 
@@ -215,7 +214,6 @@ int gate_mode(int flags) {   // 0 auto, 1 pipe, 2 pp
         const char* e = getenv("MCGMIL_GATE");
         if (e && strcmp(e, "pipe") == 0) return 1;
         if (e && strcmp(e, "pp") == 0) return 2;
-        if (e && strcmp(e, "w4") == 0) return 3;   // timing study only (mcgmil_gate_w4.h)
         return -1;
     }();
     if (env >= 0) return env;
@@ -244,26 +242,11 @@ int dispatch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
                : launch_gate_pipe<E, PPW, MAXC, false, false>(gp, s);
 }
 
-template <int MAXC>
-int launch_gate_w4(const mcgmil::GateParams& gp, hipStream_t s) {
-    auto* k = &mcgmil::gate_w4_kernel<MAXC>;
-    const long long tiles = (gp.total_samples + mcgmil::kPipeBM - 1) / mcgmil::kPipeBM;
-    if (tiles == 0) return MCGMIL_OK;
-    if (gp.uniform_rows <= 0)
-        if (int rc = launch_plan(gp, mcgmil::kPipeBM, s)) return rc;
-    hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(mcgmil::kW4Threads), mcgmil::w4_lds_bytes<MAXC>(), s, gp);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_w4_kernel launch");
-}
-
 template <typename E, int MAXC>
 int dispatch_gate_maxc(const mcgmil::GateParams& gp, int L, int dtype, int flags, hipStream_t s) {
     const bool pipe_ok = L % 64 == 0;          // the pipelined K loop is unrolled by two steps
     if constexpr (sizeof(E) == 2) {
         const int mode = gate_mode(flags);
-        if (mode == 3 && pipe_ok && !gp.keep_feat && gp.G > 1 && gp.G == gp.C && (gp.D / 16) % 4 == 0 &&
-            gp.P == 4 * mcgmil::kW4Waves)
-            return launch_gate_w4<MAXC>(gp, s);
         if (pipe_ok && mode != 1) {
             if (gp.P <= 2 * mcgmil::kPPWaves) return dispatch_gate_pp<8, 2, MAXC>(gp, s);
             if (mode == 2 && gp.P <= 4 * mcgmil::kPPWaves) return dispatch_gate_pp<4, 4, MAXC>(gp, s);

@@ -22,9 +22,6 @@ for s in ${STEPS:-fusednew smoke fused all bench}; do
         cfg5) step bench_cfg5 600 python bench.py --workload cfg5 --steps 5 --warmup 2 --no-cpu-baseline ;;
         profcfg5) rm -rf "$OUT/prof_cfg5"; step rocprof_cfg5 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg5" -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 2 --warmup 1 --no-cpu-baseline
               find "$OUT/prof_cfg5" -name "*kernel_trace.csv" -exec cp {} "$OUT/kernel_trace_cfg5.csv" \; ;;
-        w4) step w4_parity 600 env MCGMIL_GATE=w4 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rf --timeout 300 --timeout-method thread -k "bf16 or cfg3 or cfg4_ragged"
-            step w4_time 300 env MCGMIL_GATE=w4 PROBE_BAGS=512 python -u scripts/probe_fused.py
-            step pipe_time 300 env MCGMIL_GATE=pipe PROBE_BAGS=512 python -u scripts/probe_fused.py ;;
         parity) step pytest_parity 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fused.py -m gpu -x -q -rf --timeout 300 --timeout-method thread ;;
         bench) step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
         bench16) step bench16 600 python bench.py --bags 16 --no-cpu-baseline ;;
