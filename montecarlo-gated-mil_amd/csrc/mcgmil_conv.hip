@@ -444,6 +444,28 @@ __device__ __forceinline__ uint32_t swz_lin(int p, int c) {     // swz() for a p
     return (uint32_t)p * kRowBytes + (uint32_t)((c ^ ((p >> 1) & 7)) << 4);
 }
 
+// Fragment column c (lane & 15) of a halo kernel holds tile pixel frag_px(c) of its 16: the
+// ds_read_b128 lane groups pair columns {0-3, 12-15} at chunk kq with columns 4-11 at kq ^ 1, so the
+// former take the even pixels and the latter the odd ones. With the swizzle above every tap's read
+// of 16 contiguous patch pixels is then conflict-free; a fragment that wraps an output row reads
+// 2-way (with contiguous columns layers 1 / 2 averaged 1.71 / 1.81 LDS cycles per group, now
+// 1.14 / 1.43). Outputs are the same per pixel; only the BatchNorm statistics' per-lane summation
+// order follows the columns.
+__device__ __forceinline__ int frag_px(int c) { return c < 4 ? 2 * c : c < 12 ? 2 * c - 7 : 2 * c - 16; }
+
+// The halo kernels' swz_lin(pp + toff, kq) for the 9 taps of a fragment, without re-deriving
+// the swizzle from the pixel index each time: with pa = pp * 128 and pb = pp << 3 kept per tile and
+// the tap's scalar toff, the address is pa + 128 toff + (((pb + 8 toff) & 0x70) ^ 16 kq) -- three
+// VALU (add, bitop3, add3); the second K half (kq + 4, slot ^ 4) is the same offset with bit 6
+// flipped. (conv3x3c64_kernel<STATS, XF> keeps swz_lin: it spills with the extra live registers.)
+struct PatchPx {
+    uint32_t pa, pb;
+};
+__device__ __forceinline__ PatchPx patch_px(int pp) { return {(uint32_t)pp * kRowBytes, (uint32_t)pp << 3}; }
+__device__ __forceinline__ uint32_t tap_addr(PatchPx q, int toff, uint32_t kq16) {
+    return q.pa + (uint32_t)toff * kRowBytes + (((q.pb + ((uint32_t)toff << 3)) & 0x70u) ^ kq16);
+}
+
 struct HaloGeom {
     ConvGeom g;
     int WP;         // W + 2 (padded row width)
@@ -460,6 +482,9 @@ template <bool STATS, bool XF>
 __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom hg) {
     const ConvGeom& g = hg.g;
     constexpr int FI = 2, FJ = 4, KSTEPS = 18;          // wave: 64 pixels x 32 channels
+    // tap_addr (fewer VALU per fragment read) unless STATS and XF both hold registers: that
+    // instantiation spills with it
+    constexpr bool kTapAddr = !(STATS && XF);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -488,7 +513,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
     int dqr[FJ];      // this lane's output pixel offset in the tile per fragment: rows << 16 | cols
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
-        const int d = wm * 64 + j * 16 + (lane & 15), q = d / g.OW;
+        const int d = wm * 64 + j * 16 + frag_px(lane & 15), q = d / g.OW;
         dqr[j] = (q << 16) | (d - q * g.OW);
     }
     const int p0 = wave * 8 + (lane >> 3);       // first patch pixel this lane DMAs
@@ -589,6 +614,9 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
             pp[j] = (dn * HP + oh - oh0) * WP + ow;
             if (pp[j] + 2 * WP + 2 >= hg.patch_px) pp[j] = 0;
         }
+        PatchPx pq[FJ];
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) pq[j] = patch_px(pp[j]);
         f32x4 acc[FJ][FI];
 #pragma unroll
         for (int j = 0; j < FJ; ++j)
@@ -597,12 +625,19 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
             const int toff = (tap / 3) * WP + (tap % 3);
+            uint32_t ad[FJ];        // kTapAddr: the tap's K-half-0 addresses (half 1: bit 6 flipped)
+            if constexpr (kTapAddr)
+#pragma unroll
+                for (int j = 0; j < FJ; ++j) ad[j] = tap_addr(pq[j], toff, (uint32_t)(lane >> 4) << 4);
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
-                const int kq = ks * 4 + (lane >> 4);
                 bf16x8 xf[FJ];
 #pragma unroll
-                for (int j = 0; j < FJ; ++j) xf[j] = *reinterpret_cast<const bf16x8*>(Lp + swz_lin(pp[j] + toff, kq));
+                for (int j = 0; j < FJ; ++j) {
+                    const uint32_t a = kTapAddr ? (ks ? ad[j] ^ 64u : ad[j])
+                                                : swz_lin(pp[j] + toff, ks * 4 + (lane >> 4));
+                    xf[j] = *reinterpret_cast<const bf16x8*>(Lp + a);
+                }
 #pragma unroll
                 for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -613,7 +648,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
         const bool full = m0 + kBM <= g.M, first = t == t0;
 #pragma unroll
         for (int j = 0; j < FJ; ++j) {
-            const int m = m0 + wm * 64 + j * 16 + (lane & 15);
+            const int m = m0 + wm * 64 + j * 16 + frag_px(lane & 15);
             __bf16* dst = g.y + (size_t)(m < g.M ? m : 0) * 64 + wn * 32 + 4 * (lane >> 4);
             if (full) store_fragment<FI, STATS, false>(acc[j], dst, true, first && j == 0, st);
             else store_fragment<FI, STATS, true>(acc[j], dst, m < g.M, first && j == 0, st);
@@ -752,10 +787,10 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
     int dqr[FJ];      // this lane's output pixel offset in the tile per fragment: rows << 16 | cols
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
-        const int d = wm * WM + j * 16 + (lane & 15), q = d / g.OW;
+        const int d = wm * WM + j * 16 + frag_px(lane & 15), q = d / g.OW;
         dqr[j] = (q << 16) | (d - q * g.OW);
     }
-    int pp[FJ];
+    PatchPx pq[FJ];
     auto tile_setup = [&](int tm) {
         const int m0 = tm * kBM;
         const int n0 = m0 / OHW, r0m = m0 - n0 * OHW, oh0 = r0m / g.OW, ow0 = r0m - oh0 * g.OW;
@@ -770,8 +805,9 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
                 oh -= g.OH;
                 ++dn;
             }
-            pp[j] = (dn * HP + oh - oh0) * WP + ow;         // rows past M: a finite patch row
-            if (pp[j] + 2 * WP + 2 >= hg.patch_px) pp[j] = 0;
+            int pp = (dn * HP + oh - oh0) * WP + ow;         // rows past M: a finite patch row
+            if (pp + 2 * WP + 2 >= hg.patch_px) pp = 0;
+            pq[j] = patch_px(pp);
         }
     };
 
@@ -818,21 +854,34 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
             const unsigned char* A = patch0 + pbuf * PATCH;
             const unsigned char* B = wst0 + (s & 1) * WSTAGE;
             const int toff = (tap / 3) * WP + (tap % 3);
+            uint32_t ad[FJ];
+#pragma unroll
+            for (int j = 0; j < FJ; ++j) ad[j] = tap_addr(pq[j], toff, (uint32_t)(lane >> 4) << 4);
+            // K half 1's fragments are read before half 0's MFMAs (the scheduler barriers keep
+            // that order)
+            bf16x8 wf[2][FI], xf[2][FJ];
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 const int kq = ks * 4 + (lane >> 4);
-                bf16x8 wf[FI], xf[FJ];
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < FI; ++i)
-                    wf[i] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WN + i * 16 + (lane & 15), kq));
+                    wf[ks][i] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WN + i * 16 + (lane & 15), kq));
 #pragma unroll
-                for (int j = 0; j < FJ; ++j) xf[j] = *reinterpret_cast<const bf16x8*>(A + swz_lin(pp[j] + toff, kq));
+                for (int j = 0; j < FJ; ++j)
+                    xf[ks][j] = *reinterpret_cast<const bf16x8*>(A + (ks ? ad[j] ^ 64u : ad[j]));
+                if (ks == 0) continue;
 #pragma unroll
-                for (int i = 0; i < FI; ++i)
+                for (int h = 0; h < 2; ++h) {
+                    if (h == 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int j = 0; j < FJ; ++j)
-                        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[j][i], 0, 0, 0);
+                    for (int i = 0; i < FI; ++i)
+#pragma unroll
+                        for (int j = 0; j < FJ; ++j)
+                            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[h][i], xf[h][j], acc[j][i], 0, 0, 0);
+                }
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
         // XF: piece tap - 2 of the patch being loaded has landed (the wait above retired it)
         if (XF && more_patch && tap >= 2) xform(tap - 2);
@@ -841,7 +890,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
             const bool full = (tm + 1) * kBM <= g.M, first = tm == tm0;
 #pragma unroll
             for (int j = 0; j < FJ; ++j) {
-                const int m = tm * kBM + wm * WM + j * 16 + (lane & 15);
+                const int m = tm * kBM + wm * WM + j * 16 + frag_px(lane & 15);
                 __bf16* dst = g.y + (size_t)(m < g.M ? m : 0) * g.Cout + tn * BN + wn * WN + 4 * (lane >> 4);
                 if (full) store_fragment<FI, STATS, false>(acc[j], dst, true, first && j == 0, st);
                 else store_fragment<FI, STATS, true>(acc[j], dst, m < g.M, first && j == 0, st);

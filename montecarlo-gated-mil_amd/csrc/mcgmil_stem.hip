@@ -178,6 +178,27 @@ __global__ __launch_bounds__(256) void stem_prep_kernel(const StemGeom g, int KS
     (void)KS;
 }
 
+// The epilogue's reads of the wave's LDS scratch are inline asm: the compiler's wait-count pass
+// treats an LDS read after the staging's LDS-DMA as a possible alias and puts an s_waitcnt vmcnt(0)
+// in front of it, which drains the next tile's staging at the first fragment and the previous
+// fragment's output stores at every later one (the same hazard as bn_slot in mcgmil_conv.hip).
+// The scratch is written and read by one wave only, and LDS serves a wave's operations in order.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)p);
+}
+__device__ __forceinline__ u32x4 lds_read16(const void* p) {
+    u32x4 u;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(u) : "v"(lds_addr(p)) : "memory");
+    return u;
+}
+__device__ __forceinline__ void lds_wait(u32x4& a, u32x4& b) {     // names the values read: no use moves above
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b)::"memory");
+}
+__device__ __forceinline__ void lds_wait(u32x4& a, u32x4& b, u32x4& c) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c)::"memory");
+}
+
 // HP (the ResNet 3x3 / 2 / pad 1 max-pool, OW even): the epilogue also takes the horizontal
 // 3-wide, stride-2 maximum of each row and stores only that, [N, OH, OW / 2, 64] -- half the
 // activation bytes written here and read by the pooling pass (bn_vpool_kernel), which takes the
@@ -310,17 +331,16 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
                 if (HP) {
                     // pooled pixel 8 f + hj = max over fragment pixels 2 hj - 1 (the carry from the
                     // previous fragment when hj = 0; padding when f = 0), 2 hj, 2 hj + 1
-                    auto px = [&](int pp) {
-                        uint4 u = __builtin_bit_cast(uint4, *reinterpret_cast<const bf16x8*>(
-                                                                 scratch + pp * 64 + ((hc ^ (pp & 7)) << 3)));
-                        u.x ^= hflip[0]; u.y ^= hflip[1]; u.z ^= hflip[2]; u.w ^= hflip[3];
-                        return u;
-                    };
-                    const uint4 u0 = px(2 * hj), u1 = px(2 * hj + 1);
-                    uint4 um = u0;
-                    bool three = hj > 0 || f > 0;
-                    if (hj > 0) um = px(2 * hj - 1);
-                    else if (f > 0) um = *reinterpret_cast<const uint4*>(carry + 8 * hc);
+                    auto px = [&](int pp) { return scratch + pp * 64 + ((hc ^ (pp & 7)) << 3); };
+                    const u32x4 flip = {hflip[0], hflip[1], hflip[2], hflip[3]};
+                    // pixel 2 hj - 1: the scratch, or (hj = 0) the carry, stored sign-adjusted
+                    u32x4 u0 = lds_read16(px(2 * hj)), u1 = lds_read16(px(2 * hj + 1));
+                    u32x4 um = lds_read16(hj > 0 ? px(2 * hj - 1) : carry + 8 * hc);
+                    lds_wait(u0, u1, um);
+                    u0 ^= flip;
+                    u1 ^= flip;
+                    if (hj > 0) um ^= flip;
+                    const bool three = hj > 0 || f > 0;
                     const uint32_t w0[4] = {u0.x, u0.y, u0.z, u0.w}, w1[4] = {u1.x, u1.y, u1.z, u1.w},
                                    wm[4] = {um.x, um.y, um.z, um.w};
                     uint32_t o[4];
@@ -335,19 +355,22 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
                         o[d] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xFFFF0000u);   // exact
                     }
                     asm volatile("" ::: "memory");
-                    if (hj == 7) *reinterpret_cast<uint4*>(carry + 8 * hc) = u1;   // pixel 15, sign-adjusted
+                    if (hj == 7) *reinterpret_cast<u32x4*>(carry + 8 * hc) = u1;   // pixel 15, sign-adjusted
                     const int pw = 8 * f + hj;
                     if (pw < PW)
                         *reinterpret_cast<uint4*>(g.y + (((size_t)n * g.OH + oh) * PW + pw) * kCout + 8 * hc) =
                             make_uint4(o[0], o[1], o[2], o[3]);
                 } else {
+                    const int pp0 = lane >> 3, c = lane & 7;
+                    u32x4 v[2];
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int pp = (lane >> 3) + 8 * h, c = lane & 7;
-                        const bf16x8 v = *reinterpret_cast<const bf16x8*>(scratch + pp * 64 + ((c ^ (pp & 7)) << 3));
-                        if (16 * f + pp < g.OW)
-                            *reinterpret_cast<bf16x8*>(yrow + (size_t)(16 * f + pp) * kCout + 8 * c) = v;
-                    }
+                    for (int h = 0; h < 2; ++h)
+                        v[h] = lds_read16(scratch + (pp0 + 8 * h) * 64 + ((c ^ (pp0 & 7)) << 3));
+                    lds_wait(v[0], v[1]);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                        if (16 * f + pp0 + 8 * h < g.OW)
+                            *reinterpret_cast<u32x4*>(yrow + (size_t)(16 * f + pp0 + 8 * h) * kCout + 8 * c) = v[h];
                 }
                 asm volatile("" ::: "memory");
             }

@@ -6,7 +6,7 @@
 # `rocprofv3 --list-avail` (taken once into $OUT/avail.txt) is skipped, not run.
 # Summaries: scripts/pmc_summary.py.
 set -u
-OUT=gpurun_out/pmc
+OUT=${PMC_OUT:-gpurun_out/pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 CMD=${PMC_CMD:-"python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"}

@@ -6,7 +6,10 @@ mcgmil_fused.hip compiled with the library's own flags (mcgmil/_build.py; hipcc 
 * the two-kernel path's gate kernel (gate_pipe_kernel, bf16 operands, separate heads, Philox masks)
   and the shared-heads kernel fit the register file without scratch spills, at two waves per SIMD;
 * so does the launch bench.py times (gate_fused_kernel, bf16 separate heads; mcgmil_fused.hip with
-  its own flags), and it has no packed-fp32 VALU either.
+  its own flags), and it has no packed-fp32 VALU either;
+* the halo convolutions of the config-5 backbone (conv3x3c64_kernel, conv3x3_halo_kernel; every
+  STATS / input-BN instantiation) have no scratch: they run one 8-wave workgroup per CU at the
+  register limit, and a spill would put scratch traffic into the tap loop.
 """
 import os
 import re
@@ -84,3 +87,17 @@ def test_fused_kernel_fits_without_spills(fused_asm):
     assert not re.findall(r"^\s*(v_pk_(?:fma|add|mul)_f32)\b", fused_asm, flags=re.M)
     assert kernel_meta(fused_asm, FUSED, "private_seg_size") == 0
     assert kernel_meta(fused_asm, FUSED, "num_vgpr") + kernel_meta(fused_asm, FUSED, "num_agpr") <= 256
+
+
+@pytest.fixture(scope="module")
+def conv_asm(tmp_path_factory):
+    return _asm(tmp_path_factory, "mcgmil_conv.hip")
+
+
+def test_halo_conv_kernels_fit_without_spills(conv_asm):
+    syms = set(re.findall(r"\.set (_ZN12_GLOBAL__N_1\d+conv3x3(?:c64|_halo)_kernelILb[01]ELb[01]E\w*)\.private_seg_size",
+                          conv_asm))
+    assert len(syms) == 8, syms
+    for sym in syms:
+        assert kernel_meta(conv_asm, sym, "private_seg_size") == 0, sym
+        assert kernel_meta(conv_asm, sym, "num_vgpr") + kernel_meta(conv_asm, sym, "num_agpr") <= 512, sym
