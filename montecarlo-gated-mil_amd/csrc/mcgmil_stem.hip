@@ -13,7 +13,7 @@
 //
 // Persistent workgroups (2 per CU) walk a contiguous range of 4-output-row tiles; one wave per
 // output row, 7 pixel fragments x 4 channel fragments per row. The 3 x 13 staged input rows of
-// the next tile are loaded by LDS-DMA (global_load_lds_dword, no registers) into the other half
+// the next tile are loaded by LDS-DMA (buffer_load_dword ... lds, no registers) into the other half
 // of a double-buffered LDS image while this tile computes (one barrier per tile); all 6 x 4 weight fragments
 // stay in registers for the whole kernel. LDS row pitch = 16 (mod 64) dwords and channel plane
 // = k rows (mod 64), so the four K chunks of a read hit disjoint bank groups.
@@ -58,7 +58,6 @@ struct StemGeom {
     const bf16x8* w;
     __bf16* y;
     const __bf16* shift;
-    const uint32_t* zero;   // 64 zero dwords (padding source of the LDS-DMA staging)
     float* part;
     const float* gamma;     // HP: the BN weight (its signs), or NULL
     int N, Cin, H, W, OH, OW, k, pad, P;
@@ -149,13 +148,12 @@ __global__ void pack_stem_weights_kernel(const T* __restrict__ w, int Cin, int k
     }
 }
 
-// Zeroes the staging's padding source and, with batch statistics, writes the BatchNorm shift
-// row: the convolution at pixel (0, OH/2, OW/2), fp32, rounded to bf16 (any value near the
-// channel mean keeps the shifted sums well conditioned; all partials share it).
+// With batch statistics: the BatchNorm shift row, the convolution at pixel (0, OH/2, OW/2), fp32,
+// rounded to bf16 (any value near the channel mean keeps the shifted sums well conditioned; all
+// partials share it).
 __global__ __launch_bounds__(256) void stem_prep_kernel(const StemGeom g, int KS, int stats) {
     __shared__ float red[4][kCout];
     const int tid = threadIdx.x, c = tid & 63, part = tid >> 6;
-    if (tid < kCout) const_cast<uint32_t*>(g.zero)[tid] = 0u;
     if (!stats) return;
     const int oh = g.OH / 2, ow = g.OW / 2, e = g.P - g.pad;
     const __bf16* wp = reinterpret_cast<const __bf16*>(g.w);
@@ -178,10 +176,11 @@ __global__ __launch_bounds__(256) void stem_prep_kernel(const StemGeom g, int KS
     (void)KS;
 }
 
-// The epilogue's reads of the wave's LDS scratch are inline asm: the compiler's wait-count pass
+// The epilogue's reads and writes of the wave's LDS scratch are inline asm: the compiler's wait-count pass
 // treats an LDS read after the staging's LDS-DMA as a possible alias and puts an s_waitcnt vmcnt(0)
-// in front of it, which drains the next tile's staging at the first fragment and the previous
-// fragment's output stores at every later one (the same hazard as bn_slot in mcgmil_conv.hip).
+// in front of it (and of an LDS write), which drains the next tile's staging at the first fragment
+// and the previous fragment's output stores at every later one (the same hazard as bn_slot in
+// mcgmil_conv.hip).
 // The scratch is written and read by one wave only, and LDS serves a wave's operations in order.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
@@ -191,6 +190,22 @@ __device__ __forceinline__ u32x4 lds_read16(const void* p) {
     u32x4 u;
     asm volatile("ds_read_b128 %0, %1" : "=v"(u) : "v"(lds_addr(p)) : "memory");
     return u;
+}
+__device__ __forceinline__ void lds_write8(void* p, uint32_t lo, uint32_t hi) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr(p)), "v"(u32x2{lo, hi}) : "memory");
+}
+__device__ __forceinline__ void lds_write16(void* p, u32x4 v) {
+    asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+// 4 bytes per lane from a buffer straight into LDS at the wave-uniform base + 4 * lane (the
+// builtin only exists in the device pass)
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t voff, uint32_t soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 4, voff, soff, 0, 0);
+#else
+    (void)r; (void)lds; (void)voff; (void)soff;
+#endif
 }
 __device__ __forceinline__ void lds_wait(u32x4& a, u32x4& b) {     // names the values read: no use moves above
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b)::"memory");
@@ -208,7 +223,8 @@ __device__ __forceinline__ void lds_wait(u32x4& a, u32x4& b, u32x4& c) {
 template <int KS, bool STATS, bool HP>
 __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, p = lane & 15;
+    const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, p = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: the staging math is scalar
     const int buf_dw = g.Cin * g.plane;
     const int t0 = (int)((long long)blockIdx.x * g.tiles / gridDim.x);
     const int t1 = (int)((long long)(blockIdx.x + 1) * g.tiles / gridDim.x);
@@ -239,9 +255,19 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
         }
     }
 
-    // staging by LDS-DMA (global_load_lds_dword: no registers): wave w stages rows sr = w + kTH * it
-    // of the Cin x RR image, one 64-dword piece per instruction; lanes outside the image read the
-    // zero row, lanes past the row's dwords land in its pitch padding
+    // staging by LDS-DMA (buffer_load_dword ... lds: no registers): wave w stages rows
+    // sr = w + kTH * it of the Cin x RR image, one 64-dword piece per instruction. The lane's column
+    // offset of each piece is fixed for the kernel (coff); rows outside the image and columns
+    // outside the row read past the buffer's range, i.e. zeros (offsets >= 2^31 > x_bytes, no
+    // wrap: the row base is < 2^31 too); lanes past the row's dwords land in its pitch padding.
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(g.x, g.x_bytes);
+    constexpr int kPieces = (kMaxWd + 63) / 64;
+    uint32_t coff[kPieces];
+#pragma unroll
+    for (int d = 0; d < kPieces; ++d) {
+        const int gd = 64 * d + lane - (g.P >> 1);  // global dword of the row: columns 2 gd, 2 gd + 1
+        coff[d] = gd >= 0 && 2 * gd < g.W ? 4u * (uint32_t)gd : 0x80000000u;
+    }
     const int nsr = g.Cin * g.RR;
     auto stage = [&](int t, int buf) {
         const int n = t / g.TPI, oh0 = (t - n * g.TPI) * kTH;
@@ -254,15 +280,13 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
             }
             const int ih = 2 * oh0 - g.pad + rr;
             const bool rok = ih >= 0 && ih < g.H;
-            const uint32_t* row = reinterpret_cast<const uint32_t*>(g.x) +
-                                  (size_t)((n * g.Cin + ci) * g.H + (rok ? ih : 0)) * (g.W >> 1);
+            const uint32_t rowb = rok ? (uint32_t)((n * g.Cin + ci) * g.H + ih) * (uint32_t)(g.W * 2) : 0u;
             uint32_t* dst = L + ci * g.plane + rr * g.pitch;
-            for (int d0 = 0; d0 < g.wd; d0 += 64) {
-                const int gd = d0 + lane - (g.P >> 1);  // global dword of the row: columns 2 gd, 2 gd + 1
-                const bool ok = rok && gd >= 0 && 2 * gd < g.W;
-                const uint32_t* src = ok ? row + gd : g.zero + lane;
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                                 (__attribute__((address_space(3))) void*)(dst + d0), 4, 0, 0);
+#pragma unroll
+            for (int d = 0; d < kPieces; ++d) {
+                if (64 * d >= g.wd) break;
+                const uint32_t vo = rok ? coff[d] : 0x80000000u;
+                dma4(xr, dst + 64 * d, vo, rowb);
             }
         }
     };
@@ -308,23 +332,30 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
                 // epilogue: round, transpose the 16 pixels x 64 channels through the wave's LDS
                 // scratch (pixel rows of 128 B, 16-B chunks XOR-swizzled by pixel) and store
                 // each pixel row as 16-B pieces, 1 KiB contiguous per wave-instruction
-                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                // the rounded outputs as bf16 pairs (channels 4 (q) + 2 h, + 1 of fragment row i): stored
+                // to the scratch, and read back out of the same registers for the statistics
+                typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
                 const bool valid = ow < g.OW;
+                uint32_t pk[4][2];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    bf16x4 o;
 #pragma unroll
-                    for (int v = 0; v < 4; ++v) o[v] = (__bf16)acc[i][v];
+                    for (int h = 0; h < 2; ++h)
+                        pk[i][h] = __builtin_bit_cast(uint32_t, bf16x2{(__bf16)acc[i][2 * h], (__bf16)acc[i][2 * h + 1]});
                     const int c = 2 * i + (q >> 1);
-                    *reinterpret_cast<bf16x4*>(scratch + p * 64 + ((c ^ (p & 7)) << 3) + ((q & 1) << 2)) = o;
-                    if (STATS && valid) {
+                    lds_write8(scratch + p * 64 + ((c ^ (p & 7)) << 3) + ((q & 1) << 2), pk[i][0], pk[i][1]);
+                }
+                if (STATS && valid) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
 #pragma unroll
                         for (int v = 0; v < 4; ++v) {
-                            const float d = (float)o[v] - sh[4 * i + v];
+                            const uint32_t u = pk[i][v >> 1];
+                            const float y = __uint_as_float((v & 1) ? (u & 0xFFFF0000u) : (u << 16));
+                            const float d = y - sh[4 * i + v];
                             S[4 * i + v] += d;
                             SS[4 * i + v] = fmaf(d, d, SS[4 * i + v]);
                         }
-                    }
                 }
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
@@ -355,7 +386,7 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const StemGeom g
                         o[d] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xFFFF0000u);   // exact
                     }
                     asm volatile("" ::: "memory");
-                    if (hj == 7) *reinterpret_cast<u32x4*>(carry + 8 * hc) = u1;   // pixel 15, sign-adjusted
+                    if (hj == 7) lds_write16(carry + 8 * hc, u1);   // pixel 15, sign-adjusted
                     const int pw = 8 * f + hj;
                     if (pw < PW)
                         *reinterpret_cast<uint4*>(g.y + (((size_t)n * g.OH + oh) * PW + pw) * kCout + 8 * hc) =
@@ -442,7 +473,7 @@ Carve carve(const mcgmil_stem_args* a, const Geometry& G) {
         c.conv = off;
         off += al256((size_t)G.g.N * G.OH * G.OW * kCout * 2);
     }
-    c.shift = off;          // 64 bf16 shift row, then 64 zero dwords at +128
+    c.shift = off;          // 64 bf16 shift row
     off += 512;
     c.part = off;
     off += al256((size_t)c.grid * 2 * kCout * sizeof(float));
@@ -513,7 +544,6 @@ int mcgmil_stem_forward(const mcgmil_stem_args* a, void* stream) {
     g.w = static_cast<const bf16x8*>(a->w);
     g.y = a->pool_kernel > 0 ? reinterpret_cast<__bf16*>(ws + c.conv) : static_cast<__bf16*>(a->y);
     g.shift = reinterpret_cast<const __bf16*>(ws + c.shift);
-    g.zero = reinterpret_cast<const uint32_t*>(ws + c.shift + 128);
     g.part = reinterpret_cast<float*>(ws + c.part);
     g.gamma = a->gamma;
     // the ResNet pool (3 x 3, stride 2, pad 1) on an even width: horizontal half in the epilogue
@@ -522,7 +552,7 @@ int mcgmil_stem_forward(const mcgmil_stem_args* a, void* stream) {
     const bool unsplit = hp_env ? !strcmp(hp_env, "0") : a->flags == MCGMIL_STEM_POOL_UNSPLIT;
     const bool hp = a->pool_kernel == 3 && a->pool_stride == 2 && a->pool_pad == 1 && G.OW % 2 == 0 && !unsplit;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(stem_prep_kernel, dim3(1), dim3(256), 0, s, g, G.KS, (int)stats);
+    if (stats) hipLaunchKernelGGL(stem_prep_kernel, dim3(1), dim3(256), 0, s, g, G.KS, 1);
     switch (G.KS) {
         case 1: launch_conv<1>(g, c.grid, G.lds, stats, hp, s); break;
         case 2: launch_conv<2>(g, c.grid, G.lds, stats, hp, s); break;
