@@ -101,7 +101,8 @@ typedef struct mcgmil_conv_args {
     const void* w;              /* packed bf16 [out_channels, kernel_h, kernel_w, in_channels] */
     void* y;                    /* bf16 [batch, OH, OW, out_channels] */
     float* stats;               /* optional out: BatchNorm statistics of y, [parts][3][out_channels]
-                                   = (count, mean, M2) of the bf16 outputs per workgroup row,
+                                   = (count, mean, M2) of the bf16 outputs per workgroup row
+                                   (per pixel stream for the 1x1 streaming kernel),
                                    parts = mcgmil_conv_stats_parts() (0 when the layer's
                                    kernel emits none: then stats is ignored and the BN computes
                                    its statistics from y); hand them to mcgmil_batchnorm_act as
@@ -123,8 +124,10 @@ typedef struct mcgmil_conv_args {
 
 /* mcgmil_conv_args.flags */
 enum mcgmil_conv_flags {
-    MCGMIL_CONV_TILE_AUTO = 0,     /* the measured-fastest kernel per layer shape */
-    MCGMIL_CONV_TILE_NOHALO = 1,   /* no halo-patch kernels (generic LDS-DMA kernel everywhere) */
+    MCGMIL_CONV_TILE_AUTO = 0,     /* the measured-fastest kernel per layer shape (1x1 / stride 2
+                                      from 64 channels: a streaming kernel) */
+    MCGMIL_CONV_TILE_NOHALO = 1,   /* no halo-patch or streaming kernels (generic LDS-DMA kernel
+                                      everywhere) */
     MCGMIL_CONV_TILE_SMALL = 2,    /* 256 x 128 tiles where auto would take 256 x 256 */
     MCGMIL_CONV_TILE_BIG512 = 3    /* 512 x 128 tiles on 128-channel layers */
 };

@@ -907,10 +907,140 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
                                              g.Cout, tn * BN);
 }
 
+// ---- conv1x1_kernel: 1x1 / stride s / no padding, Cin = 32 KS (the plan uses it for 64 -> 128), a
+// streaming kernel without LDS stages (conv_dma_kernel moved these at 2.3-3.6 TB/s: one K step per
+// tile leaves its stage ring and 8-byte epilogue stores exposed). A wave owns 32 output channels --
+// its weights stay in registers -- and walks 16-pixel fragments of one pixel stream: a fragment's
+// Cin input channels are loaded by buffer loads straight into MFMA B fragments (16 B per lane; the
+// next fragment's are in flight during this one's MFMAs), and the outputs leave as one 16-byte
+// store per lane. For that the weight rows are permuted: row r of fragment i is channel
+// 32 cb + 8 (r >> 2) + 4 i + (r & 3), so a lane's two accumulators hold 8 consecutive channels.
+// The CB = Cout / 32 waves of a pixel stream are neighbours in the grid and share its input in L2.
+// Statistics (STATS): one (n, mean, M2) row per pixel stream for each wave's 32 channels.
+constexpr int k1x1Threads = 256;
+template <int KS, bool STATS>
+__global__ __launch_bounds__(k1x1Threads) void conv1x1_kernel(const ConvGeom g) {
+    constexpr int FI = 2;
+    const int lane = threadIdx.x & 63, q = lane >> 4, c16 = lane & 15;
+    const int wid = (int)blockIdx.x * (k1x1Threads / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int CB = g.Cout / 32, PS = (int)gridDim.x * (k1x1Threads / 64) / CB;
+    const int cb = wid % CB, ps = wid / CB;
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(g.x, g.x_bytes);
+
+    bf16x8 wf[KS][FI];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int i = 0; i < FI; ++i) {
+            const int ch = 32 * cb + 8 * (c16 >> 2) + 4 * i + (c16 & 3);
+            wf[s][i] = *reinterpret_cast<const bf16x8*>(g.w + (size_t)ch * (KS * 32) + s * 32 + 8 * q);
+        }
+    LaneStats<4 * FI> st;
+    if (STATS) st.init();
+
+    const int OHW = g.OH * g.OW, nfrag = (g.M + 15) >> 4;
+    auto load = [&](int f, bf16x8 (&xf)[KS]) {
+        // the fragment's first pixel in scalar math (f is wave-uniform), then the lane's column
+        const int m0 = 16 * f, n0 = m0 / OHW, r0 = m0 - n0 * OHW, oh0 = r0 / g.OW;
+        int n = n0, oh = oh0, ow = r0 - oh0 * g.OW + c16;
+        if (m0 + c16 >= g.M) {          // past the last pixel: load the last one (not stored)
+            n = g.N - 1;
+            oh = g.OH - 1;
+            ow = g.OW - 1;
+        }
+        while (ow >= g.OW) {
+            ow -= g.OW;
+            ++oh;
+        }
+        while (oh >= g.OH) {
+            oh -= g.OH;
+            ++n;
+        }
+        const uint32_t off = ((uint32_t)((n * g.H + oh * g.stride) * g.W + ow * g.stride) * (uint32_t)(KS * 32) +
+                              8u * (uint32_t)q) * 2u;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            xf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, off + 64u * s, 0, 0));
+    };
+    bf16x8 xa[KS], xb[KS];
+    int f = ps;
+    if (f < nfrag) load(f, xa);
+    bool first = true;
+    while (f < nfrag) {
+        const int fn = f + PS;
+        if (fn < nfrag) load(fn, xb);
+        f32x4 acc[FI];
+#pragma unroll
+        for (int i = 0; i < FI; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int i = 0; i < FI; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s][i], xa[s], acc[i], 0, 0, 0);
+        const int m = 16 * f + c16;
+        const bool valid = m < g.M;
+        typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+        uint32_t pk[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+            pk[h] = __builtin_bit_cast(uint32_t, bf16x2{(__bf16)acc[h >> 1][2 * (h & 1)], (__bf16)acc[h >> 1][2 * (h & 1) + 1]});
+        if (valid)
+            __builtin_nontemporal_store(u32x4{pk[0], pk[1], pk[2], pk[3]},
+                                        reinterpret_cast<u32x4*>(g.y + (size_t)m * g.Cout + 32 * cb + 8 * q));
+        if (STATS) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t u = pk[c >> 1];
+                const float x = __uint_as_float((c & 1) ? (u & 0xFFFF0000u) : (u << 16));
+                if (first) st.set_x0(c, x);
+                float d = x - st.x0(c);
+                d = valid ? d : 0.f;
+                st.S[c] += d;
+                st.SS[c] = fmaf(d, d, st.SS[c]);
+            }
+            st.n += valid ? 1.f : 0.f;
+        }
+        first = false;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) xa[s] = xb[s];
+        f = fn;
+    }
+    if (STATS) {
+        // the lane's channel c (0..7) is 32 cb + 8 q + c: merge the 16 pixel lanes, lanes c16 = 0 write
+        float n = st.n, mean[8], M2[8];
+        const float rn = n > 0.f ? 1.f / n : 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            mean[c] = st.x0(c) + st.S[c] * rn;
+            M2[c] = fmaxf(st.SS[c] - st.S[c] * st.S[c] * rn, 0.f);
+            if (!(n > 0.f)) mean[c] = M2[c] = 0.f;
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            float mb[8], M2b[8];
+            const float nb = __shfl_xor(n, o, 64);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                mb[c] = __shfl_xor(mean[c], o, 64);
+                M2b[c] = __shfl_xor(M2[c], o, 64);
+            }
+            chan_merge<8>(n, mean, M2, nb, mb, M2b);
+        }
+        if (c16 == 0) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const int ch = 32 * cb + 8 * q + c;
+                g.stats[((size_t)ps * 3 + 0) * g.Cout + ch] = n;
+                g.stats[((size_t)ps * 3 + 1) * g.Cout + ch] = mean[c];
+                g.stats[((size_t)ps * 3 + 2) * g.Cout + ch] = M2[c];
+            }
+        }
+    }
+}
+
 // ---- launch plan: which kernel, its grid and the statistics rows (Gm x 3 x Cout floats)
 struct Plan {
     int kind = 0;          // 1: halo 64 -> 64, 2: dma 256 x 128, 3: dma 256 x 64, 4: halo, streamed
-                           // weights, 5: dma 512 x 128, 6: dma 256 x 256
+                           // weights, 5: dma 512 x 128, 6: dma 256 x 256, 7: 1x1 streaming
     int grid = 0;
     int parts = 0;         // statistics rows
     size_t lds = 0;
@@ -975,6 +1105,25 @@ Plan make_plan(ConvGeom& g, int flags) {
             p.hg = hg;
             return p;
         }
+    }
+    // 1x1 / stride 2 from 64 channels (layer 2's downsample): the streaming kernel, unless the policy
+    // pins the dma tiles. Measured at config 5 (scripts/probe_conv.py, k = 916): 64 -> 128 82.6 ->
+    // 59.3 us; but 128 -> 256 40.2 -> 54.5 and 256 -> 512 33.1 -> 56.7 (8 / 16 waves per pixel stream
+    // re-read its input from L2, and a stream holds only 5-11 fragments), so those stay on the dma tiles
+    if (policy == MCGMIL_CONV_TILE_AUTO && g.KH == 1 && g.KW == 1 && g.pad == 0 && g.stride == 2 && g.Cin == 64 &&
+        !g.in_ab) {
+        const int CB = g.Cout / 32, waves = 32 * cus;    // 8 waves per SIMD
+        int ps = waves / CB;
+        const int nfrag = (g.M + 15) / 16;
+        if (ps > nfrag) ps = nfrag;
+        if (ps < 1) ps = 1;
+        // 4 waves per workgroup, the CB waves of a pixel stream adjacent: CB * ps waves in all
+        while ((CB * ps) % 4) ++ps;
+        p.kind = 7;
+        p.grid = CB * ps / 4;
+        p.parts = ps;
+        g.Gm = ps;
+        return p;
     }
     const int BN = g.Cout % 128 == 0 ? 128 : 64;
     g.tiles_n = g.Cout / BN;
@@ -1057,6 +1206,13 @@ int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
                              : (stats ? (xf ? conv3x3_halo_kernel<true, true> : conv3x3_halo_kernel<true, false>)
                                       : (xf ? conv3x3_halo_kernel<false, true> : conv3x3_halo_kernel<false, false>));
         return launch_lds(k, grid, block, p.lds, s, hg);
+    }
+    if (p.kind == 7) {
+        const dim3 b1(k1x1Threads);
+        auto k = stats ? conv1x1_kernel<2, true> : conv1x1_kernel<2, false>;     // Cin = 64
+        hipLaunchKernelGGL(k, grid, b1, 0, s, g);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "conv1x1_kernel launch");
     }
     if (p.kind == 2)
         return stats ? launch_lds(conv_dma_kernel<256, 128, 4, 3, true>, grid, block, p.lds, s, g)

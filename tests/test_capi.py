@@ -246,6 +246,14 @@ def test_conv_stats_parts_and_validation(hip_lib):
     assert p.value == 0
     assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(256, 256, 3, 1, 1, 14, flags=2)), ctypes.byref(p)) == 0
     assert p.value >= 1
+    # 1x1 / stride 2 from 64 channels (layer 2's downsample): the streaming kernel's pixel streams,
+    # one row each, at most one per 16-pixel fragment; 256 -> 512 stays on the 256 x 256 dma tiles
+    assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 128, 1, 2, 0, 56)), ctypes.byref(p)) == 0
+    assert 1 <= p.value <= (8 * 28 * 28 + 15) // 16
+    assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 128, 1, 2, 0, 4)), ctypes.byref(p)) == 0
+    assert p.value == 2                                                  # 32 pixels: 2 fragments
+    assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(256, 512, 1, 2, 0, 14)), ctypes.byref(p)) == 0
+    assert p.value == 0
     assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 64, 3, 1, 1, flags=4)), ctypes.byref(p)) == -1
     assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 64, 3, 1, 1, reserved=1)), ctypes.byref(p)) == -1
 

@@ -39,6 +39,11 @@ SHAPES = [
     (4, 128, 25, 20, 128, 3, 1, 1),
     (2, 192, 17, 30, 256, 3, 1, 1),
     (1, 128, 6, 80, 128, 3, 1, 1),
+    # 1x1 / stride 2 streaming kernel: layer 3's shape at odd sizes (pixels not a multiple of the
+    # 16-pixel fragment), 192 output channels (6 waves per pixel stream), a single image
+    (3, 128, 13, 11, 256, 1, 2, 0),
+    (2, 64, 9, 7, 192, 1, 2, 0),
+    (1, 256, 14, 14, 512, 1, 2, 0),
 ]
 
 
@@ -144,6 +149,8 @@ STATS_SHAPES = [
     (2, 128, 10, 10, 128, 3, 1, 1, 4.0),
     (4, 128, 25, 20, 128, 3, 1, 1, 0.0),
     (2, 192, 17, 30, 256, 3, 1, 1, 2.0),
+    (3, 128, 13, 11, 256, 1, 2, 0, 2.0),
+    (2, 64, 28, 28, 128, 1, 2, 0, 0.0),
 ]
 
 
@@ -187,10 +194,11 @@ def test_conv_bn_act_fused_statistics(cuda, shape, residual):
     assert torch.all(err <= bound), float((err - bound).max())
 
 
-def test_conv_statistics_deterministic(cuda):
+@pytest.mark.parametrize("cin,cout,k,s,p", [(128, 256, 3, 1, 1), (64, 128, 1, 2, 0)])
+def test_conv_statistics_deterministic(cuda, cin, cout, k, s, p):
     from mcgmil.features import conv2d
-    conv = _layer(128, 256, 3, 1, 1, cuda, 7)
-    x = torch.randn(6, 128, 28, 28, device=cuda).relu_().bfloat16().contiguous(memory_format=torch.channels_last)
+    conv = _layer(cin, cout, k, s, p, cuda, 7)
+    x = torch.randn(6, cin, 28, 28, device=cuda).relu_().bfloat16().contiguous(memory_format=torch.channels_last)
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
         y1, p1 = conv2d(conv, x, stats=True)
         y2, p2 = conv2d(conv, x, stats=True)
