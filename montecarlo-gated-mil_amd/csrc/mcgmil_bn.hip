@@ -54,6 +54,12 @@ __device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
 #ifndef MCGMIL_BN_NT
 #define MCGMIL_BN_NT 1
 #endif
+#ifndef MCGMIL_BN_UNROLL
+#define MCGMIL_BN_UNROLL 2
+#endif
+#ifndef MCGMIL_BN_MAXBLOCKS
+#define MCGMIL_BN_MAXBLOCKS 4096
+#endif
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void load8s(const __bf16* p, float (&v)[8]) {
 #if MCGMIL_BN_NT
@@ -300,18 +306,19 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const E* x, const E*
         store8s(y + i * 8, o);
     };
     long long i = i0;
-    for (; i + stride < nvec; i += 2 * stride) {
-        float v[8], w[8], r[8], q[8];
-        load8s(x + i * 8, v);
-        load8s(x + (i + stride) * 8, w);
-        if (RES) {
-            load8s(res + i * 8, r);
-            load8s(res + (i + stride) * 8, q);
+    // U vectors per thread and iteration, all loads issued before any arithmetic
+    constexpr int U = MCGMIL_BN_UNROLL;
+    for (; i + (U - 1) * stride < nvec; i += U * stride) {
+        float v[U][8], r[U][8];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            load8s(x + (i + u * stride) * 8, v[u]);
+            if (RES) load8s(res + (i + u * stride) * 8, r[u]);
         }
-        one(i, v, r);
-        one(i + stride, w, q);
+#pragma unroll
+        for (int u = 0; u < U; ++u) one(i + u * stride, v[u], r[u]);
     }
-    if (i < nvec) {
+    for (; i < nvec; i += stride) {
         float v[8], r[8];
         load8s(x + i * 8, v);
         if (RES) load8s(res + i * 8, r);
@@ -414,6 +421,58 @@ __global__ __launch_bounds__(kThreads) void bn_vpool_kernel(const __bf16* __rest
     }
 }
 
+// The same pass with a thread per (image, pooled column, 8-channel group): it walks the column's
+// Ho output rows top to bottom, so each input row is read once -- the row 2 oh + 1 that pooled rows
+// oh and oh + 1 share is carried in registers (bn_vpool_kernel reads it twice, from L2 if lucky).
+template <bool RELU>
+__global__ __launch_bounds__(kThreads) void bn_vpool_col_kernel(const __bf16* __restrict__ x, __bf16* __restrict__ y,
+                                                                int H, int Wp, int Ho, long long ncol, int C,
+                                                                const float* __restrict__ ab) {
+    const int CG = C >> 3;
+    const long long rs = (long long)Wp * C;          // elements per (pooled-width) row
+    for (long long col = (long long)blockIdx.x * kThreads + threadIdx.x; col < ncol;
+         col += (long long)gridDim.x * kThreads) {
+        const int cg = (int)(col % CG);
+        const long long t = col / CG;
+        const int pw = (int)(t % Wp);
+        const long long n = t / Wp;
+        float a[8], b[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            a[j] = ab[cg * 8 + j];
+            b[j] = ab[C + cg * 8 + j];
+        }
+        const __bf16* xc = x + (n * H * Wp + pw) * (long long)C + cg * 8;
+        __bf16* yc = y + (n * Ho * Wp + pw) * (long long)C + cg * 8;
+        float carry[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) carry[j] = -INFINITY;   // row -1: padding
+#pragma unroll 2
+        for (int oh = 0; oh < Ho; ++oh) {
+            const int r0 = 2 * oh, r1 = 2 * oh + 1;
+            float v0[8], v1[8];
+            if (r0 < H) load8s(xc + r0 * rs, v0);
+            else
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v0[j] = -INFINITY;
+            if (r1 < H) load8s(xc + r1 * rs, v1);
+            else
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v1[j] = -INFINITY;
+            float o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float m = fmaxf(fmaxf(carry[j], v0[j]), v1[j]);
+                carry[j] = v1[j];
+                const float v = signbit(a[j]) ? -m : m;
+                const float r = fmaf(v, a[j], b[j]);
+                o[j] = RELU ? fmaxf(r, 0.f) : r;
+            }
+            store8s(yc + oh * rs, o);
+        }
+    }
+}
+
 int pooled_dim(int size, const mcgmil_bn_args* a) {
     return (size + 2 * a->pool_pad - a->pool_kernel) / a->pool_stride + 1;
 }
@@ -486,7 +545,7 @@ void launch_apply(const mcgmil_bn_args* a, const float* ab, hipStream_t s) {
     // blocks: a multiple of CG / gcd(CG, 256) so that every thread keeps its channel group
     const int unit = CG / std::gcd(CG, kThreads);
     long long want = (nvec + 2LL * kThreads - 1) / (2LL * kThreads);
-    if (want > 4096) want = 4096;
+    if (want > MCGMIL_BN_MAXBLOCKS) want = MCGMIL_BN_MAXBLOCKS;
     long long blocks = (want + unit - 1) / unit * unit;
     hipLaunchKernelGGL((bn_apply_kernel<E, RELU, RES, RESBN>), dim3((unsigned)blocks), dim3(kThreads), 0, s,
                        static_cast<const E*>(a->x), static_cast<const E*>(a->residual),
@@ -506,9 +565,21 @@ int apply_step(const mcgmil_bn_args* a, const float* ab, hipStream_t s, bool hpo
         long long want = (nvec + kThreads - 1) / kThreads;
         if (want > 8192) want = 8192;
         const long long blocks = (want + unit - 1) / unit * unit;
-        auto k = a->relu ? bn_vpool_kernel<true> : bn_vpool_kernel<false>;
-        hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kThreads), 0, s, static_cast<const __bf16*>(a->x),
-                           static_cast<__bf16*>(a->y), a->height, Wp, Ho, nvec, C, ab);
+#ifndef MCGMIL_VPOOL_COL
+#define MCGMIL_VPOOL_COL 0
+#endif
+        if (MCGMIL_VPOOL_COL && a->pool_kernel == 3 && a->pool_stride == 2 && a->pool_pad == 1) {
+            const long long ncol = (long long)a->batch * Wp * (C / 8);
+            long long cb = (ncol + kThreads - 1) / kThreads;
+            if (cb > 8192) cb = 8192;
+            auto k = a->relu ? bn_vpool_col_kernel<true> : bn_vpool_col_kernel<false>;
+            hipLaunchKernelGGL(k, dim3((unsigned)cb), dim3(kThreads), 0, s, static_cast<const __bf16*>(a->x),
+                               static_cast<__bf16*>(a->y), a->height, Wp, Ho, ncol, C, ab);
+        } else {
+            auto k = a->relu ? bn_vpool_kernel<true> : bn_vpool_kernel<false>;
+            hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kThreads), 0, s, static_cast<const __bf16*>(a->x),
+                               static_cast<__bf16*>(a->y), a->height, Wp, Ho, nvec, C, ab);
+        }
         const hipError_t e = hipGetLastError();
         return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "batchnorm vertical pool launch");
     }
