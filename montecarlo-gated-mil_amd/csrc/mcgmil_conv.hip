@@ -23,6 +23,8 @@
 //                      registers, each tile's input rows DMA'd once into a zero-padded LDS patch
 //                      that all 9 taps read (the generic kernel fetches every pixel 9 times and
 //                      is L2-bound on these layers).
+//   (and conv3x3_halo_kernel, the same patch idea with streamed weights for Cin >= 128, and
+//   conv1x1_kernel, a streaming 1x1 / stride-2 kernel without LDS stages for 64 -> 128.)
 // Optional BatchNorm statistics (a->stats, conv_dma_kernel only): each lane keeps running sums of its channels' bf16
 // outputs around its first value; at the end the lanes and waves of a workgroup are merged
 // (Chan's pairwise update, fixed order) into one (count, mean, M2) block per workgroup, which
