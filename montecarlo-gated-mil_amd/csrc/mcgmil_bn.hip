@@ -55,7 +55,7 @@ __device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
 #define MCGMIL_BN_NT 1
 #endif
 #ifndef MCGMIL_BN_UNROLL
-#define MCGMIL_BN_UNROLL 2
+#define MCGMIL_BN_UNROLL 2      // 4 (and 8,192 or 2,048 blocks) measured within 2% (profiles/r04/bn_ab/)
 #endif
 #ifndef MCGMIL_BN_MAXBLOCKS
 #define MCGMIL_BN_MAXBLOCKS 4096
@@ -566,7 +566,7 @@ int apply_step(const mcgmil_bn_args* a, const float* ab, hipStream_t s, bool hpo
         if (want > 8192) want = 8192;
         const long long blocks = (want + unit - 1) / unit * unit;
 #ifndef MCGMIL_VPOOL_COL
-#define MCGMIL_VPOOL_COL 0
+#define MCGMIL_VPOOL_COL 1      // measured: the stem layer 0.725-0.733 -> 0.682 ms at k = 916
 #endif
         if (MCGMIL_VPOOL_COL && a->pool_kernel == 3 && a->pool_stride == 2 && a->pool_pad == 1) {
             const long long ncol = (long long)a->batch * Wp * (C / 8);
