@@ -76,6 +76,8 @@ enum mcgmil_flags {
                                     pairs (separate heads), gate_pp_kernel for <= 8 (shared) */
     MCGMIL_GATE_PIPE = 1 << 2,   /* always gate_pipe_kernel (one 8-wave workgroup per CU) */
     MCGMIL_GATE_PP = 2 << 2,     /* gate_pp_kernel (two 4-wave workgroups per CU) where it applies */
+    MCGMIL_GATE_ROW = 3 << 2,    /* rowgate_scores_kernel (one wave per SIMD, each wave owns whole
+                                    rows; bf16, D % 32 == 0, <= 16 gate column blocks of 32) */
     MCGMIL_GATE_MASK = 3 << 2
 };
 

@@ -12,4 +12,7 @@ long long fused_regions(const mcgmil::GateParams& gp, long long total_rows, int 
 int launch_gate_fused(const mcgmil::GateParams& gp, bool bf16, int ppw, int maxc, bool one,
                       long long total_rows, hipStream_t s);
 
+// rowgate_fused_kernel<G, D/32, maxc> (mcgmil_rowgate.h; bf16, D = 128, G = 1 or 2).
+int launch_rowgate_fused(const mcgmil::GateParams& gp, int maxc, long long total_rows, hipStream_t s);
+
 }  // namespace mcgmil_detail

@@ -21,7 +21,7 @@ MCGMIL_U16 = 3
 ABI_VERSION = 3
 # mcgmil_args.flags (include/mcgmil.h enum mcgmil_flags)
 PATH_FLAGS = {"auto": 0, "fused": 1, "two_kernel": 2}
-GATE_FLAGS = {"auto": 0, "pipe": 1 << 2, "pp": 2 << 2}
+GATE_FLAGS = {"auto": 0, "pipe": 1 << 2, "pp": 2 << 2, "row": 3 << 2}
 
 EXPORTED = (
     "mcgmil_abi_version", "mcgmil_args_size", "mcgmil_last_error", "mcgmil_workspace_size",
