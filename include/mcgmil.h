@@ -47,8 +47,9 @@
 extern "C" {
 #endif
 
-#define MCGMIL_ABI_VERSION 3   /* 2: mcgmil_args.flags (path selection); 3: mcgmil_conv_args.flags,
-                                  mcgmil_stem_args.flags (mcgmil_features.h) */
+#define MCGMIL_ABI_VERSION 4   /* 2: mcgmil_args.flags (path selection); 3: mcgmil_conv_args.flags,
+                                  mcgmil_stem_args.flags (mcgmil_features.h); 4: MCGMIL_GATE_ROW and
+                                  the row-gate weight stream in the packed weights */
 
 enum mcgmil_status {
     MCGMIL_OK = 0,
@@ -63,8 +64,8 @@ enum mcgmil_dtype { MCGMIL_F32 = 0, MCGMIL_BF16 = 1 };
 
 /* mcgmil_args.flags: which launch path mcgmil_gate_softmax_pool / mcgmil_mcdo_forward take. All
  * paths give bitwise the same A and Y (tests/test_gpu_fused.py); the choice is performance only.
- * The environment variables MCGMIL_FUSED (0 | 1 | auto) and MCGMIL_GATE (pipe | pp), when set,
- * override the flags (A/B timing of an unmodified caller). */
+ * The environment variables MCGMIL_FUSED (0 | 1 | auto) and MCGMIL_GATE (pipe | pp | row), when
+ * set, override the flags (A/B timing of an unmodified caller); they are read once per process. */
 enum mcgmil_flags {
     MCGMIL_PATH_AUTO = 0,        /* fused launch for bf16 batches of equal-size bags with >= 16,384
                                     regions, else the two kernels */

@@ -269,15 +269,28 @@ int device_cus() {
 }
 
 // The reference's heads: C = 2 classes, D = 128, shared (G = 1) or separate (G = 2) gates; L a
-// multiple of 32 of at least 64 (K steps of 16, two peeled at each end of a tile).
+// multiple of 64 of at least 128 (K steps of 16 in groups of 4 ring slots, four peeled at each end
+// of a tile).
 bool rowgate_applies(const mcgmil::GateParams& gp) {
-    return gp.Wr && gp.D == 128 && (gp.G == 1 || gp.G == 2) && gp.L % 32 == 0 && gp.L >= 64 && gp.C <= 4;
+    return gp.Wr && gp.D == 128 && (gp.G == 1 || gp.G == 2) && gp.L % 64 == 0 && gp.L >= 128 && gp.C <= 4;
+}
+
+// The LDS-DMA weight stream (asm operand reads) wherever the kernel fits without spills; the
+// replayed-mask separate-heads kernel with 4 classes stages the weights through registers
+// (tests/test_codegen_guard.py checks both). MCGMIL_RG_SAFE_ALL (timing builds): staging everywhere.
+template <int G, int MAXC, bool REPLAY>
+constexpr bool rowgate_dma() {
+#ifdef MCGMIL_RG_SAFE_ALL
+    return false;
+#else
+    return !(REPLAY && G == 2 && MAXC == 4);
+#endif
 }
 
 template <int G, int DB, int MAXC, bool REPLAY>
 int launch_rowgate(const mcgmil::GateParams& gp, hipStream_t s) {
     constexpr int NCB = 2 * G * DB;
-    auto* k = &mcgmil::rowgate_scores_kernel<G, DB, MAXC, REPLAY>;
+    auto* k = &mcgmil::rowgate_scores_kernel<G, DB, MAXC, REPLAY, rowgate_dma<G, MAXC, REPLAY>()>;
     if (int rc = mcgmil_detail::raise_lds_limit(reinterpret_cast<const void*>(k), "rowgate_scores_kernel LDS limit"))
         return rc;
     const long long tiles = (gp.total_samples + mcgmil::kRgRows - 1) / mcgmil::kRgRows;
@@ -333,11 +346,17 @@ int dispatch_gate(const mcgmil::GateParams& gp, int L, int dtype, int flags, hip
 // applies, MCGMIL_PATH_TWO_KERNEL never; MCGMIL_FUSED=1 / 0 / auto in the environment overrides.
 constexpr long long kFusedMinRegions = 16384;
 
-int fused_mode(int flags) {   // -1 auto, 0 off, 1 on (env read per call: tests switch it in one process)
-    const char* e = getenv("MCGMIL_FUSED");
-    if (e && strcmp(e, "1") == 0) return 1;
-    if (e && strcmp(e, "0") == 0) return 0;
-    if (e && strcmp(e, "auto") == 0) return -1;
+int fused_mode(int flags) {   // -1 auto, 0 off, 1 on
+    // MCGMIL_FUSED overrides the flags; read once per process (in-process callers switch paths
+    // through args->flags)
+    static const int env = [] {
+        const char* e = getenv("MCGMIL_FUSED");
+        if (e && strcmp(e, "1") == 0) return 1;
+        if (e && strcmp(e, "0") == 0) return 0;
+        if (e && strcmp(e, "auto") == 0) return -1;
+        return -2;
+    }();
+    if (env != -2) return env;
     const int path = flags & MCGMIL_PATH_MASK;
     return path == MCGMIL_PATH_FUSED ? 1 : path == MCGMIL_PATH_TWO_KERNEL ? 0 : -1;
 }

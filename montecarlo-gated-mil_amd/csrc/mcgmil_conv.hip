@@ -1072,13 +1072,16 @@ ConvGeom geom_of(const mcgmil_conv_args* a) {
 }
 
 // The tile policy: args->flags (mcgmil_conv_flags), or MCGMIL_CONV_TILE=nohalo|small|big512 in the
-// environment, which overrides the flags (A/B timing of an unmodified caller)
+// environment, which overrides the flags (A/B timing of an unmodified caller; read once per process)
 int tile_policy(int flags) {
-    const char* e = getenv("MCGMIL_CONV_TILE");
-    if (e && !strcmp(e, "nohalo")) return MCGMIL_CONV_TILE_NOHALO;
-    if (e && !strcmp(e, "small")) return MCGMIL_CONV_TILE_SMALL;
-    if (e && !strcmp(e, "big512")) return MCGMIL_CONV_TILE_BIG512;
-    return flags;
+    static const int env = [] {
+        const char* e = getenv("MCGMIL_CONV_TILE");
+        if (e && !strcmp(e, "nohalo")) return (int)MCGMIL_CONV_TILE_NOHALO;
+        if (e && !strcmp(e, "small")) return (int)MCGMIL_CONV_TILE_SMALL;
+        if (e && !strcmp(e, "big512")) return (int)MCGMIL_CONV_TILE_BIG512;
+        return -1;
+    }();
+    return env >= 0 ? env : flags;
 }
 
 Plan make_plan(ConvGeom& g, int flags) {

@@ -87,7 +87,13 @@ int launch_maxc(const mcgmil::GateParams& gp, int ppw, bool one, long long total
 template <int G, int MAXC>
 int launch_row(const mcgmil::GateParams& gp, long long total_rows, hipStream_t s) {
     constexpr int NCB = 2 * G * 4;
-    auto* k = &mcgmil::rowgate_fused_kernel<G, 4, MAXC>;
+    auto* k = &mcgmil::rowgate_fused_kernel<G, 4, MAXC,
+#ifdef MCGMIL_RG_SAFE_ALL
+                                          false
+#else
+                                          true
+#endif
+                                          >;   // LDS-DMA where it fits without spills
     if (int rc = raise_lds_limit(reinterpret_cast<const void*>(k), "rowgate_fused_kernel LDS limit")) return rc;
     constexpr int cap = mcgmil::rg_fused_cap<MAXC>();
     if (gp.uniform_rows <= 0) {

@@ -10,9 +10,10 @@
 //     B fragment of v_mfma_f32_32x32x16_bf16. No feature staging through LDS, no feature barrier,
 //     and every keep decision is drawn once (the same counters as gate_pipe_kernel: {l>>3, n, t, bag}).
 //   - the weights are the A operands: NCB column blocks of 32 (V and U of each 32-wide d block,
-//     gate by gate) stream through a 2-slot LDS ring, one 16-deep K step (NCB KiB) per slot;
-//     each wave stages NCB/4 of the 1-KiB fragments of a step (register staging, one barrier per
-//     K step) and reads all NCB of them: each weight byte leaves L2 once per CU per tile.
+//     gate by gate) stream through a 4-slot LDS ring, one 16-deep K step (NCB KiB) per slot,
+//     filled by LDS-DMA three steps ahead (each wave issues NCB/4 of the 1-KiB pieces of a step:
+//     no staging registers, no ds_write); each wave reads all NCB fragments of step s+1 while it
+//     runs step s's MFMAs, one barrier per K step: each weight byte leaves L2 once per CU per tile.
 //   - the classifier projection z = X k_c: v_dot2_f32_bf16 on the lane's own 8 features per K
 //     step against k_c from an LDS table (a 32-row MFMA tile for 2 classes would cost 1/16 of the
 //     matrix pipe, and 16 accumulator registers more than the AGPR file holds).
@@ -31,7 +32,7 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 constexpr int kRgWaves = 4;
 constexpr int kRgThreads = kRgWaves * kWave;
 constexpr int kRgRows = 32 * kRgWaves;      // rows of a tile
-constexpr int kRgSlots = 2;                 // weight ring slots (K steps)
+constexpr int kRgSlots = 4;                 // weight ring slots (K steps): one being read, two landing, one free
 
 // Column blocks of the row-gate weight stream: V and U of each 32-wide d block of each gate.
 __host__ __device__ inline int rg_ncb(int G, int D) { return D % 32 == 0 ? 2 * G * D / 32 : 0; }
@@ -42,8 +43,10 @@ __host__ __device__ inline size_t rg_stream_bytes(int L, int G, int D) {
 }
 // Followed by the classifier table [4][L] bf16 (rows >= C zero).
 __host__ __device__ inline size_t rg_cls_bytes(int L) { return (size_t)4 * L * 2; }
+// Only heads the row kernel runs (D = 128, one or two gates, L a multiple of 64, >= 128) get one.
 __host__ __device__ inline size_t rg_packed_bytes(int L, int G, int D) {
-    return rg_ncb(G, D) ? rg_stream_bytes(L, G, D) + rg_cls_bytes(L) : 0;
+    const bool fits = D == 128 && (G == 1 || G == 2) && L % 64 == 0 && L >= 128;
+    return fits ? rg_stream_bytes(L, G, D) + rg_cls_bytes(L) : 0;
 }
 
 template <typename E>
@@ -80,7 +83,7 @@ __host__ __device__ inline size_t rg_ktab_bytes(int L) { return (size_t)MAXC * L
 __host__ __device__ inline size_t rg_head_bytes(int G, int C, int D) { return (size_t)(2 * G + C) * D * 4; }
 template <int NCB, int MAXC>
 __host__ __device__ inline size_t rg_lds_bytes(int L, int G, int C, int D) {
-    return rg_ring_bytes<NCB>() + rg_ktab_bytes<MAXC>(L) + rg_head_bytes(G, C, D);
+    return rg_ring_bytes<NCB>() + rg_ktab_bytes<MAXC>(L) + rg_head_bytes(G, MAXC, D);   // wa zero-padded to MAXC rows
 }
 
 // One lane's row of a tile.
@@ -90,6 +93,7 @@ struct RgLane {
     uint32_t inval;       // ~0: padding row (stages zeros, stores nothing)
     long long R;          // flattened (bag, t, n) row (replay masks, outputs)
     int bag;
+    const unsigned char* kf;   // replay: the row's keep_feat bytes + (l >> 5) (row 0's for padding)
 };
 
 // Row R of the flattened space -> its lane record (the mapping of fill_row_table).
@@ -136,6 +140,7 @@ __device__ __forceinline__ RgLane rg_lane_flat(const GateParams& p, long long R,
     rl.inval = hrow >= 0 ? 0u : 0xFFFFFFFFu;
     rl.R = R;
     rl.bag = bag;
+    rl.kf = p.keep_feat ? p.keep_feat + (size_t)(hrow >= 0 ? R : 0) * (p.L >> 3) + hl : nullptr;
     return rl;
 }
 
@@ -144,7 +149,7 @@ template <bool REPLAY>
 __device__ __forceinline__ bf16x8 rg_stage(const GateParams& p, const RgLane& rl, uint4 h, int s) {
     const int hl = (threadIdx.x >> 5) & 1;
     if constexpr (REPLAY) {
-        const uint32_t kb = rl.inval ? 0u : p.keep_feat[(size_t)rl.R * (p.L >> 3) + 2 * s + hl];
+        const uint32_t kb = (uint32_t)rl.kf[2 * s] & ~rl.inval;
         uint4 v = h;
         v.x &= ((kb & 1u) ? 0x0000FFFFu : 0u) | ((kb & 2u) ? 0xFFFF0000u : 0u);
         v.y &= ((kb & 4u) ? 0x0000FFFFu : 0u) | ((kb & 8u) ? 0xFFFF0000u : 0u);
@@ -162,9 +167,6 @@ __device__ __forceinline__ bf16x8 rg_stage(const GateParams& p, const RgLane& rl
     }
 }
 
-__device__ __forceinline__ uint4 rg_hload(const RgLane& rl, int s) {
-    return *reinterpret_cast<const uint4*>(rl.h + 32 * s);
-}
 
 __device__ __forceinline__ f32x16 mma32(bf16x8 a, bf16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -181,13 +183,62 @@ __device__ __forceinline__ float rg_dot8(bf16x8 x, uint4 k, float acc) {
     return acc;
 }
 
-// One-time setup of a workgroup: head vectors and classifier table into LDS, the ring primed
-// with K steps 0 (in LDS slot 0) and 1 (in flight into staging set 1). Visible after the caller's
-// barrier. LDS: [ring][classifier rows 0..MAXC-1][bv', bu', wa].
-template <int NCB, int MAXC>
+// LDS byte address of a pointer into the dynamic LDS.
+__device__ __forceinline__ uint32_t rg_lds(const unsigned char* p) {
+    return (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const unsigned char*)p);
+}
+
+// 16 bytes per lane from the weight stream into LDS at the wave-uniform `lds` + 16 * lane (LDS-DMA).
+// The builtin only exists in the device pass; the host pass must still see a body.
+__device__ __forceinline__ void rg_dma(__amdgpu_buffer_rsrc_t r, unsigned char* lds, uint32_t voff, uint32_t soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+#else
+    (void)r; (void)lds; (void)voff; (void)soff;
+#endif
+}
+
+// LDS reads of the ring and the classifier table as inline asm: the compiler's wait-count pass
+// treats a ds_read after an LDS-DMA as a possible alias and would put an s_waitcnt vmcnt(0) in
+// front of it, draining the weight DMAs in flight. The reads are waited for explicitly (the
+// end-of-step barrier's lgkmcnt(0), which names their registers).
+typedef unsigned int rg_u32x4 __attribute__((ext_vector_type(4)));   // a native vector for asm operands
+template <int OFF>
+__device__ __forceinline__ rg_u32x4 rg_ds_read(uint32_t addr) {
+    rg_u32x4 v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+    return v;
+}
+// H rows are ordinary loads: the compiler's wait-count pass then orders every use (and every
+// copy) of the loaded registers after the data lands. (An inline-asm load would leave its
+// destination registers in flight where the compiler may copy or reuse them.)
+__device__ __forceinline__ uint4 rg_hload(const char* p) { return *reinterpret_cast<const uint4*>(p); }
+template <int N>
+__device__ __forceinline__ void rg_vmwait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Registers a wave carries from one K step to the next (and across tiles): the weight fragments
+// and classifier features of the next step (read during this step), X and H of the next steps,
+// and (register staging, DMA = false) the weights of steps in flight from L2.
+template <int NCB, int MAXC, bool DMA>
+struct RgPipe {
+    rg_u32x4 af[NCB];  // A fragments of the next step (complete after the step's barrier)
+    rg_u32x4 kf[MAXC]; // classifier features of the next step
+    bf16x8 x;          // X fragment of the next step
+    uint4 h;           // H of the step after it (loaded)
+    uint4 ws[DMA ? 1 : 2][NCB / 4];   // register staging: set t & 1 holds step t's pieces
+};
+
+// One-time setup of a workgroup: head vectors and classifier table into LDS, the ring's first
+// K steps (DMA: steps 0..2 by LDS-DMA into slots 0..2; register staging: steps 0..1 into slots 0..1
+// and step 2 into staging set 0). Visible after the caller's barrier.
+// LDS: [ring][classifier rows 0..MAXC-1][bv', bu', wa].
+template <int NCB, int MAXC, bool DMA>
 __device__ __forceinline__ void rg_setup(const GateParams& p, unsigned char* smem, __amdgpu_buffer_rsrc_t& wrs,
-                                         uint4 (&ws)[2][NCB / 4]) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+                                         RgPipe<NCB, MAXC, DMA>& pp) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     unsigned char* kt = smem + rg_ring_bytes<NCB>();
     float* head = reinterpret_cast<float*>(kt + rg_ktab_bytes<MAXC>(p.L));
     const size_t sbytes = rg_stream_bytes(p.L, p.G, p.D);
@@ -200,29 +251,39 @@ __device__ __forceinline__ void rg_setup(const GateParams& p, unsigned char* sme
         head[i] = p.bv[i] * kM2Log2e;
         head[GD + i] = p.bu[i] * kMLog2e;
     }
-    for (int i = tid; i < p.C * p.D; i += kRgThreads) head[2 * GD + i] = p.wa[i];
-    // steps 0 and 1 of the stream into staging sets 0 and 1; set 0 straight into slot 0
+    for (int i = tid; i < MAXC * p.D; i += kRgThreads) head[2 * GD + i] = i < p.C * p.D ? p.wa[i] : 0.f;
     const uint32_t lane_b = (uint32_t)lane * 16u;
+    if constexpr (DMA) {
 #pragma unroll
-    for (int i = 0; i < NCB / 4; ++i) {
-        const uint32_t cb = (uint32_t)(wave * (NCB / 4) + i);
-        ws[0][i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane_b, cb * 1024u, 0));
-        ws[1][i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                 wrs, lane_b, ((uint32_t)NCB + cb) * 1024u, 0));
+        for (int st = 0; st < 3; ++st)
+#pragma unroll
+            for (int i = 0; i < NCB / 4; ++i) {
+                const uint32_t cb = (uint32_t)(wave * (NCB / 4) + i);
+                rg_dma(wrs, smem + (size_t)(st * NCB + (int)cb) * 1024, lane_b, ((uint32_t)(st * NCB) + cb) * 1024u);
+            }
+        rg_vmwait<0>();
+    } else {
+#pragma unroll
+        for (int st = 0; st < 3; ++st)
+#pragma unroll
+            for (int i = 0; i < NCB / 4; ++i) {
+                const uint32_t cb = (uint32_t)(wave * (NCB / 4) + i);
+                const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                              wrs, lane_b, ((uint32_t)(st * NCB) + cb) * 1024u, 0));
+                if (st < 2) *reinterpret_cast<uint4*>(smem + (size_t)(st * NCB + (int)cb) * 1024 + lane_b) = v;
+                else pp.ws[0][i] = v;
+            }
     }
-#pragma unroll
-    for (int i = 0; i < NCB / 4; ++i)
-        *reinterpret_cast<uint4*>(smem + (size_t)(wave * (NCB / 4) + i) * 1024 + lane_b) = ws[0][i];
 }
 
 // Timing-only ablations (never in the product; wrong results): 1 no Philox/keep rule, 2 no
-// transcendentals in the epilogue, 4 no weight staging, 8 no H loads, 16 no barrier, 32 no MFMAs,
-// 64 no epilogue.
+// transcendentals in the epilogue, 4 no weight DMA, 8 no H loads, 16 no barrier, 32 no MFMAs,
+// 64 no epilogue arithmetic (accumulators kept live).
 #ifndef MCGMIL_RG_DIAG
 #define MCGMIL_RG_DIAG 0
 #endif
 
-// Scheduling of one K step: MFMA i is followed by one LDS operand read and VPM vector ops.
+// Scheduling of one K step: MFMA i is followed by VPM vector ops.
 #ifndef MCGMIL_RG_VPM
 #define MCGMIL_RG_VPM 4
 #endif
@@ -243,103 +304,188 @@ template <int V> using rg_int = std::integral_constant<int, V>;
 #define RG_STAMP(p, tile, i) do {} while (0)
 #endif
 
-// One tile's K loop. `rn` = the next tile's lane record: its first K step's X fragment and the H of
-// its second step are made during this tile's last two steps. On entry x0 = this tile's X[0] and
-// h1 = its H[1] (loaded); on return the next tile's. The weight stream continues across tiles
-// (tile i's step s is global step i*KS + s; KS is even, so slot = s & 1 and staging set = s & 1).
-// Needs KS = L/16 >= 4.
-template <int NCB, int MAXC, bool REPLAY>
+// Reads of step `s`'s A fragments (ring slot SLOT) and classifier features into pp (asm, waited
+// for at the next barrier). The ds_read offset is an immediate: one template instance per block.
+// DMA = false: ordinary LDS loads (no LDS-DMA in flight, so the compiler orders them itself).
+template <int NCB, int MAXC, bool DMA, int SLOT, int C = 0>
+__device__ __forceinline__ void rg_read_frags(RgPipe<NCB, MAXC, DMA>& pp, const unsigned char* smem, uint32_t ring_lane) {
+    if constexpr (C < NCB) {
+        if constexpr (DMA) pp.af[C] = rg_ds_read<(SLOT * NCB + C) * 1024>(ring_lane);
+        else pp.af[C] = *reinterpret_cast<const rg_u32x4*>(smem + (size_t)(SLOT * NCB + C) * 1024 + (threadIdx.x & 63) * 16);
+        rg_read_frags<NCB, MAXC, DMA, SLOT, C + 1>(pp, smem, ring_lane);
+    }
+}
+template <int NCB, int MAXC, bool DMA, int SLOT>
+__device__ __forceinline__ void rg_prefetch(RgPipe<NCB, MAXC, DMA>& pp, const unsigned char* smem, uint32_t ring_lane,
+                                            uint32_t ktab_lane, int L, int s) {
+    rg_read_frags<NCB, MAXC, DMA, SLOT>(pp, smem, ring_lane);
+    const uint32_t ka = ktab_lane + 32u * (uint32_t)s;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        if constexpr (DMA) pp.kf[c] = rg_ds_read<0>(ka + (uint32_t)(c * L * 2));
+        else pp.kf[c] = *reinterpret_cast<const rg_u32x4*>(smem + rg_ring_bytes<NCB>() + 16 * ((threadIdx.x & 63) >> 5) +
+                                                            32 * s + (size_t)c * L * 2);
+    }
+}
+
+// The prefetched registers' lgkmcnt(0) wait: one statement naming all of them, so no copy of a
+// register whose ds_read is still in flight can be placed before it.
+template <int NCB, int MAXC, bool DMA>
+__device__ __forceinline__ void rg_wait_frags(RgPipe<NCB, MAXC, DMA>& pp, bool barrier) {
+    static_assert((NCB == 16 || NCB == 8) && (MAXC == 2 || MAXC == 4), "row-gate shapes");
+#define RG_A8 "+v"(pp.af[0]), "+v"(pp.af[1]), "+v"(pp.af[2]), "+v"(pp.af[3]), "+v"(pp.af[4]), "+v"(pp.af[5]), \
+              "+v"(pp.af[6]), "+v"(pp.af[7])
+#define RG_A16 RG_A8, "+v"(pp.af[8]), "+v"(pp.af[9]), "+v"(pp.af[10]), "+v"(pp.af[11]), "+v"(pp.af[12]), \
+              "+v"(pp.af[13]), "+v"(pp.af[14]), "+v"(pp.af[15])
+#define RG_K2 "+v"(pp.kf[0]), "+v"(pp.kf[1])
+#define RG_K4 RG_K2, "+v"(pp.kf[2]), "+v"(pp.kf[3])
+    if (barrier) {
+        if constexpr (NCB == 16 && MAXC == 2) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" : RG_A16, RG_K2::"memory");
+        if constexpr (NCB == 16 && MAXC == 4) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" : RG_A16, RG_K4::"memory");
+        if constexpr (NCB == 8 && MAXC == 2) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" : RG_A8, RG_K2::"memory");
+        if constexpr (NCB == 8 && MAXC == 4) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" : RG_A8, RG_K4::"memory");
+    } else {
+        if constexpr (NCB == 16 && MAXC == 2) asm volatile("s_waitcnt lgkmcnt(0)" : RG_A16, RG_K2::"memory");
+        if constexpr (NCB == 16 && MAXC == 4) asm volatile("s_waitcnt lgkmcnt(0)" : RG_A16, RG_K4::"memory");
+        if constexpr (NCB == 8 && MAXC == 2) asm volatile("s_waitcnt lgkmcnt(0)" : RG_A8, RG_K2::"memory");
+        if constexpr (NCB == 8 && MAXC == 4) asm volatile("s_waitcnt lgkmcnt(0)" : RG_A8, RG_K4::"memory");
+    }
+#undef RG_A8
+#undef RG_A16
+#undef RG_K2
+#undef RG_K4
+}
+
+// End of a K step: (DMA) my DMA pieces of the step after next have landed (vmcnt: each step issues
+// NCB/4 DMA pieces and one H load, so the NCB/4 + 1 youngest vector-memory ops are this step's,
+// whatever order the compiler gave them); the prefetched reads and this step's ring writes are
+// complete; barrier.
+template <int NCB, int MAXC, bool DMA>
+__device__ __forceinline__ void rg_step_barrier(RgPipe<NCB, MAXC, DMA>& pp) {
+    if constexpr (DMA) rg_vmwait<NCB / 4 + 1>();
+    rg_wait_frags<NCB, MAXC, DMA>(pp, !(MCGMIL_RG_DIAG & 16));
+}
+
+// One tile's K loop over global steps; `rn` = the next tile's lane record (its X[0] and H[1] are
+// made / loaded during this tile's last steps). On entry pp holds this tile's step 0 (A fragments,
+// classifier features, X[0]) and H[1]; on return the next tile's. Step s of a tile uses ring slot
+// s % 4 (KS = L/16 is a multiple of 4). DMA: step s issues the LDS-DMA of step s + 3 (mod KS: the
+// next tile's first steps) into slot (s + 3) % 4. Register staging: step s writes step s + 2's
+// pieces (loaded a step earlier) into slot (s + 2) % 4 and loads step s + 3's. Needs KS >= 8.
+template <int NCB, int MAXC, bool REPLAY, bool DMA>
 __device__ __forceinline__ void rg_kloop(const GateParams& p, unsigned char* smem, __amdgpu_buffer_rsrc_t wrs,
-                                         const RgLane& rl, const RgLane& rn, uint4 (&ws)[2][NCB / 4],
-                                         bf16x8& x0, uint4& h1, f32x16 (&acc)[NCB], float (&zp)[MAXC]) {
+                                         const RgLane& rl, const RgLane& rn, RgPipe<NCB, MAXC, DMA>& pp,
+                                         f32x16 (&acc)[NCB], float (&zp)[MAXC]) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int KS = p.L >> 4;
     const uint32_t lane_b = (uint32_t)lane * 16u;
-    const unsigned char* ktab = smem + rg_ring_bytes<NCB>() + 16 * (lane >> 5);
+    const uint32_t ring_lane = rg_lds(smem) + lane_b;
+    const uint32_t ktab_lane = rg_lds(smem + rg_ring_bytes<NCB>()) + 16u * (uint32_t)(lane >> 5);
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) zp[c] = 0.f;
-    bf16x8 xe = x0, xo;          // X of even / odd steps
-    uint4 ho = h1, he;           // H of odd / even steps
-    // step s on slot SL = s & 1: barrier, then the step's NCB MFMAs with X[s]; meanwhile X[s+1]
-    // from H[s+1], H[s+2] and the weights of step s+2 (into staging set SL) are loaded, and set
-    // SL ^ 1 (step s+1) is written into slot SL ^ 1 at the end of the step. MODE 0: inside the
-    // tile; 1: the first step (accumulators start at zero); 2: step s+2 is the next tile's step 0;
-    // 3: steps s+1 and s+2 are the next tile's steps 0 and 1.
-    auto kstep = [&](auto sl_c, auto mode_c, int s, const bf16x8& x, bf16x8& xn, const uint4& hn1, uint4& hn2) {
+    // MODE 0: inside the tile; 1: the first step (accumulators start at zero); 2: step s+2 is the
+    // next tile's step 0; 3: steps s+1 and s+2 are the next tile's steps 0 and 1.
+    auto kstep = [&](auto sl_c, auto mode_c, int s) {
         constexpr int SL = decltype(sl_c)::value, MODE = decltype(mode_c)::value;
         constexpr bool N1 = MODE == 3, N2 = MODE >= 2;
-#if MCGMIL_RG_DIAG & 16
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
         const RgLane& l1 = N1 ? rn : rl;
         const RgLane& l2 = N2 ? rn : rl;
         const int s1 = N1 ? s + 1 - KS : s + 1, s2 = N2 ? s + 2 - KS : s + 2;
-#if MCGMIL_RG_DIAG & 8
-        hn2 = hn1;
-#else
-        hn2 = rg_hload(l2, s2);
-#endif
-        const uint32_t wstep = (uint32_t)s2 * (uint32_t)NCB * 1024u;
-#if !(MCGMIL_RG_DIAG & 4)
-#pragma unroll
-        for (int i = 0; i < NCB / 4; ++i)
-            ws[SL][i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      wrs, lane_b, wstep + (uint32_t)(wave * (NCB / 4) + i) * 1024u, 0));
-#endif
-        const unsigned char* slot = smem + (size_t)SL * NCB * 1024 + lane_b;
-        // all NCB operand reads of the step first (counted waits before each MFMA): with one
-        // register quad for every fragment the compiler serialised an LDS round trip per MFMA
-        uint4 kf[MAXC];       // the classifier rows' 8 features of this K step (before the fragments)
-#pragma unroll
-        for (int c = 0; c < MAXC; ++c) kf[c] = *reinterpret_cast<const uint4*>(ktab + (size_t)c * p.L * 2 + 32 * s);
-        bf16x8 af[NCB];
-#pragma unroll
-        for (int c = 0; c < NCB; ++c) af[c] = *reinterpret_cast<const bf16x8*>(slot + (size_t)c * 1024);
+        const int s3 = s + 3 < KS ? s + 3 : s + 3 - KS;
         __builtin_amdgcn_sched_barrier(0);
+        // this step's operands; the next step's are read into pp below
+        rg_u32x4 af[NCB];
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) af[c] = pp.af[c];
+        rg_u32x4 kf[MAXC];
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) kf[c] = pp.kf[c];
+        const bf16x8 x = pp.x;
+        const uint4 h1 = pp.h;                             // H[s+1] (issued a step ago)
+        // this step's vector-memory ops: H[s+2] and the DMA of step s+3
+#if MCGMIL_RG_DIAG & 8
+        const uint4 h2 = h1;
+#else
+        const uint4 h2 = rg_hload(l2.h + 32 * s2);
+#endif
+#if !(MCGMIL_RG_DIAG & 4)
+        if constexpr (DMA) {
+#pragma unroll
+            for (int i = 0; i < NCB / 4; ++i) {
+                const uint32_t cb = (uint32_t)(wave * (NCB / 4) + i);
+                rg_dma(wrs, smem + (size_t)(((SL + 3) & 3) * NCB + (int)cb) * 1024, lane_b,
+                       ((uint32_t)s3 * (uint32_t)NCB + cb) * 1024u);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NCB / 4; ++i) {
+                const uint32_t cb = (uint32_t)(wave * (NCB / 4) + i);
+                *reinterpret_cast<uint4*>(smem + (size_t)(((SL + 2) & 3) * NCB + (int)cb) * 1024 + lane_b) = pp.ws[SL & 1][i];
+                pp.ws[(SL + 1) & 1][i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                       wrs, lane_b, ((uint32_t)s3 * (uint32_t)NCB + cb) * 1024u, 0));
+            }
+        }
+#endif
+        rg_prefetch<NCB, MAXC, DMA, (SL + 1) & 3>(pp, smem, ring_lane, ktab_lane, p.L, N1 ? 0 : s + 1);
 #pragma unroll
         for (int c = 0; c < NCB; ++c) {
 #if MCGMIL_RG_DIAG & 32
-            acc[c][c & 15] += __builtin_bit_cast(float, (uint32_t)af[c][0] ^ 0u);
+            acc[c][c & 15] += __uint_as_float(af[c].x ^ 0u);
 #else
-            acc[c] = mma32(af[c], x, MODE == 1 ? f32x16{} : acc[c]);
+            acc[c] = mma32(__builtin_bit_cast(bf16x8, af[c]), x, MODE == 1 ? f32x16{} : acc[c]);
 #endif
         }
 #pragma unroll
-        for (int c = 0; c < MAXC; ++c) zp[c] = rg_dot8(x, kf[c], zp[c]);
+        for (int c = 0; c < MAXC; ++c) zp[c] = rg_dot8(x, __builtin_bit_cast(uint4, kf[c]), zp[c]);
+        // X[s+1] from H[s+1] (the compiler waits for the load)
 #if MCGMIL_RG_DIAG & 1
-        xn = __builtin_bit_cast(bf16x8, make_uint4(hn1.x & ~l1.inval, hn1.y, hn1.z, hn1.w ^ (uint32_t)s1));
+        pp.x = __builtin_bit_cast(bf16x8, make_uint4(h1.x & ~l1.inval, h1.y, h1.z, h1.w ^ (uint32_t)s1));
 #else
-        xn = rg_stage<REPLAY>(p, l1, hn1, s1);
+        pp.x = rg_stage<REPLAY>(p, l1, h1, s1);
 #endif
-#if !(MCGMIL_RG_DIAG & 4)
-        unsigned char* wslot = smem + (size_t)(SL ^ 1) * NCB * 1024 + lane_b;
-#pragma unroll
-        for (int i = 0; i < NCB / 4; ++i)
-            *reinterpret_cast<uint4*>(wslot + (size_t)(wave * (NCB / 4) + i) * 1024) = ws[SL ^ 1][i];
-#endif
+        pp.h = h2;
 #pragma unroll
         for (int i = 0; i < NCB; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // MFMA
             __builtin_amdgcn_sched_group_barrier(0x002, MCGMIL_RG_VPM, 0);  // VALU
         }
+        __builtin_amdgcn_sched_barrier(0);
+        rg_step_barrier<NCB, MAXC, DMA>(pp);
     };
     const rg_int<0> S0{}, M0{};
     const rg_int<1> S1{}, M1{};
-    const rg_int<2> M2{};
-    const rg_int<3> M3{};
-    kstep(S0, M1, 0, xe, xo, ho, he);
-    kstep(S1, M0, 1, xo, xe, he, ho);
-    for (int s = 2; s < KS - 2; s += 2) {
-        kstep(S0, M0, s, xe, xo, ho, he);
-        kstep(S1, M0, s + 1, xo, xe, he, ho);
+    const rg_int<2> S2{}, M2{};
+    const rg_int<3> S3{}, M3{};
+    kstep(S0, M1, 0);
+    kstep(S1, M0, 1);
+    kstep(S2, M0, 2);
+    kstep(S3, M0, 3);
+    for (int s = 4; s < KS - 4; s += 4) {
+        kstep(S0, M0, s);
+        kstep(S1, M0, s + 1);
+        kstep(S2, M0, s + 2);
+        kstep(S3, M0, s + 3);
     }
-    kstep(S0, M2, KS - 2, xe, xo, ho, he);     // H[s+2] = the next tile's H[0]
-    kstep(S1, M3, KS - 1, xo, xe, he, ho);     // X[s+1] = the next tile's X[0], H[s+2] its H[1]
-    x0 = xe;
-    h1 = ho;
+    kstep(S0, M0, KS - 4);
+    kstep(S1, M0, KS - 3);
+    kstep(S2, M2, KS - 2);     // H[s+2] = the next tile's H[0]
+    kstep(S3, M3, KS - 1);     // X[s+1] = the next tile's X[0], H[s+2] its H[1]
+}
+
+// Prologue of a workgroup's first tile: its step-0 operands and H[1] into pp (after rg_setup's
+// DMA and the caller's barrier).
+template <int NCB, int MAXC, bool REPLAY, bool DMA>
+__device__ __forceinline__ void rg_first(const GateParams& p, unsigned char* smem, const RgLane& rl,
+                                         RgPipe<NCB, MAXC, DMA>& pp) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t ring_lane = rg_lds(smem) + (uint32_t)lane * 16u;
+    const uint32_t ktab_lane = rg_lds(smem + rg_ring_bytes<NCB>()) + 16u * (uint32_t)(lane >> 5);
+    rg_prefetch<NCB, MAXC, DMA, 0>(pp, smem, ring_lane, ktab_lane, p.L, 0);
+    const uint4 h0 = rg_hload(rl.h);
+    pp.h = rg_hload(rl.h + 32);
+    pp.x = rg_stage<REPLAY>(p, rl, h0, 0);
+    rg_wait_frags<NCB, MAXC, DMA>(pp, false);
 }
 
 // The epilogue of a tile: scores, logit dropout, z; store(rl, c, logit, z) per (row, class).
@@ -353,8 +499,13 @@ __device__ __forceinline__ void rg_epilogue(const GateParams& p, const unsigned 
     constexpr int NCB = 2 * G * DB, D = 32 * DB;
     const int lane = threadIdx.x & 63, hl = lane >> 5;
 #if MCGMIL_RG_DIAG & 64
-    if (!rl.inval) store(rl, hl, acc[0][0] + acc[NCB - 1][15] + zp[0], 0.f);
-    return;
+    {   // every accumulator stays live (its MFMAs are kept), no epilogue arithmetic
+        float t = zp[0];
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) t += acc[c][c & 15];
+        if (!rl.inval) store(rl, hl, t, 0.f);
+        return;
+    }
 #endif
     const float* head = reinterpret_cast<const float*>(smem + rg_ring_bytes<NCB>() + rg_ktab_bytes<MAXC>(p.L));
     const float av_s = p.sf * kM2Log2e, au_s = p.sf * kMLog2e;
@@ -367,6 +518,9 @@ __device__ __forceinline__ void rg_epilogue(const GateParams& p, const unsigned 
     for (int g = 0; g < G; ++g) {
 #pragma unroll
         for (int db = 0; db < DB; ++db) {
+            // keeps the compiler from hoisting every d block's head-vector reads to the top (their
+            // registers, live through the whole epilogue, spill the shared-heads kernels)
+            asm volatile("" ::: "memory");
             const int cb = g * 2 * DB + 2 * db;
             float ax[16], by[16], w[MAXC][16];
 #pragma unroll
@@ -376,7 +530,7 @@ __device__ __forceinline__ void rg_epilogue(const GateParams& p, const unsigned 
                 const f32x4 bu = *reinterpret_cast<const f32x4*>(head + G * D + g * D + d0);
 #pragma unroll
                 for (int c = 0; c < MAXC; ++c) {
-                    const bool use = G == 1 ? c < p.C : c == g;
+                    const bool use = G == 1 || c == g;   // rows c >= C are zero
                     const f32x4 wq = use ? *reinterpret_cast<const f32x4*>(head + 2 * G * D + c * D + d0)
                                          : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -422,20 +576,27 @@ __device__ __forceinline__ void rg_epilogue(const GateParams& p, const unsigned 
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-    // the other lane half holds the row's other d values and other 8 features of each K step
-    float sc[MAXC];
+    // the other lane half holds the row's other d values and other 8 features of each K step;
+    // lane half hl scores classes hl, hl + 2 (selected value by value: a select between two
+    // elements of one array becomes a dynamically indexed stack array)
+    float pcs[MAXC / 2], zcs[MAXC / 2];
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-        sc[c] = (part[c][0] + part[c][1]) + (part[c][2] + part[c][3]);
-        sc[c] += __shfl_xor(sc[c], 32);
+        float sc = (part[c][0] + part[c][1]) + (part[c][2] + part[c][3]);
+        sc += __shfl_xor(sc, 32);
         z[c] = zp[c] + __shfl_xor(zp[c], 32);
+        if ((c & 1) == 0) {
+            pcs[c / 2] = sc;
+            zcs[c / 2] = z[c];
+        } else {
+            pcs[c / 2] = hl ? sc : pcs[c / 2];
+            zcs[c / 2] = hl ? z[c] : zcs[c / 2];
+        }
     }
-    // lane half hl scores classes hl, hl + 2
 #pragma unroll
     for (int c0 = 0; c0 < MAXC; c0 += 2) {
         const int c = c0 + hl;
-        const float pc = hl ? sc[c0 + 1] : sc[c0];
-        const float zc = hl ? z[c0 + 1] : z[c0];
+        const float pc = pcs[c0 / 2], zc = zcs[c0 / 2];
         if (c >= p.C || rl.inval) continue;
         bool keep;
         if constexpr (REPLAY) {
@@ -450,21 +611,21 @@ __device__ __forceinline__ void rg_epilogue(const GateParams& p, const unsigned 
 }
 
 // Two-kernel path: persistent workgroups over the 128-row tiles; logits and z to the workspace.
-template <int G, int DB, int MAXC, bool REPLAY>
+// DMA: the LDS-DMA weight stream with asm operand reads -- only for instantiations the compiler
+// fits without spills (tests/test_codegen_guard.py); else register staging, all compiler-visible.
+template <int G, int DB, int MAXC, bool REPLAY, bool DMA>
 __global__ __launch_bounds__(kRgThreads, 1) void rowgate_scores_kernel(const GateParams p, long long tiles) {
     constexpr int NCB = 2 * G * DB;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __amdgpu_buffer_rsrc_t wrs;
-    uint4 ws[2][NCB / 4];
-    rg_setup<NCB, MAXC>(p, smem, wrs, ws);
+    RgPipe<NCB, MAXC, DMA> pp;
+    rg_setup<NCB, MAXC, DMA>(p, smem, wrs, pp);
     long long tile = blockIdx.x;
     auto row_of = [&](long long tl) { return tl < tiles ? tl * kRgRows + 32 * wave + (lane & 31) : p.total_samples; };
     RgLane rl = rg_lane_flat(p, row_of(tile), tile);
-    const uint4 h0 = rg_hload(rl, 0);
-    uint4 h1 = rg_hload(rl, 1);
-    bf16x8 x0 = rg_stage<REPLAY>(p, rl, h0, 0);
     __syncthreads();
+    rg_first<NCB, MAXC, REPLAY, DMA>(p, smem, rl, pp);
     f32x16 acc[NCB];
     float zp[MAXC];
     for (; tile < tiles; tile += gridDim.x) {
@@ -472,7 +633,7 @@ __global__ __launch_bounds__(kRgThreads, 1) void rowgate_scores_kernel(const Gat
         const long long nt = tile + gridDim.x;
         const RgLane rn = rg_lane_flat(p, row_of(nt), nt);
         RG_STAMP(p, tile, 1);
-        rg_kloop<NCB, MAXC, REPLAY>(p, smem, wrs, rl, rn, ws, x0, h1, acc, zp);
+        rg_kloop<NCB, MAXC, REPLAY, DMA>(p, smem, wrs, rl, rn, pp, acc, zp);
         RG_STAMP(p, tile, 2);
         rg_epilogue<G, DB, MAXC, REPLAY>(p, smem, rl, acc, zp, [&](const RgLane& r, int c, float lg, float z) {
             p.logits[(size_t)r.R * p.C + c] = lg;
@@ -517,10 +678,11 @@ __device__ __forceinline__ RgLane rg_lane_region(const GateParams& p, const Regi
     rl.inval = hrow >= 0 ? 0u : 0xFFFFFFFFu;
     rl.R = rg.S + rho;
     rl.bag = rg.bag;
+    rl.kf = nullptr;   // the fused kernel makes its own masks
     return rl;
 }
 
-template <int G, int DB, int MAXC>
+template <int G, int DB, int MAXC, bool DMA>
 __global__ __launch_bounds__(kRgThreads, 1) void rowgate_fused_kernel(const GateParams p) {
     constexpr int NCB = 2 * G * DB;
     constexpr int CAP = rg_fused_cap<MAXC>();
@@ -532,8 +694,8 @@ __global__ __launch_bounds__(kRgThreads, 1) void rowgate_fused_kernel(const Gate
     Region rg;
     if (!decode_region(p, (int)blockIdx.x, CAP, rg)) return;   // grid rounded up (ragged bags)
     __amdgpu_buffer_rsrc_t wrs;
-    uint4 ws[2][NCB / 4];
-    rg_setup<NCB, MAXC>(p, smem, wrs, ws);
+    RgPipe<NCB, MAXC, DMA> pp;
+    rg_setup<NCB, MAXC, DMA>(p, smem, wrs, pp);
     const bool in_lds = rg.Nb <= CAP;
     float* lg_out = in_lds ? slg : p.logits;
     float* z_out = in_lds ? szz : p.zz;
@@ -542,15 +704,13 @@ __global__ __launch_bounds__(kRgThreads, 1) void rowgate_fused_kernel(const Gate
         return i < rg.ntiles ? (long long)region_tile(rg, i) * kRgRows + 32 * wave + (lane & 31) : rg.rows;
     };
     RgLane rl = rg_lane_region(p, rg, rho_of(0));
-    const uint4 h0 = rg_hload(rl, 0);
-    uint4 h1 = rg_hload(rl, 1);
-    bf16x8 x0 = rg_stage<false>(p, rl, h0, 0);
     __syncthreads();
+    rg_first<NCB, MAXC, false, DMA>(p, smem, rl, pp);
     f32x16 acc[NCB];
     float zp[MAXC];
     for (int i = 0; i < rg.ntiles; ++i) {
         const RgLane rn = rg_lane_region(p, rg, rho_of(i + 1));
-        rg_kloop<NCB, MAXC, false>(p, smem, wrs, rl, rn, ws, x0, h1, acc, zp);
+        rg_kloop<NCB, MAXC, false, DMA>(p, smem, wrs, rl, rn, pp, acc, zp);
         rg_epilogue<G, DB, MAXC, false>(p, smem, rl, acc, zp, [&](const RgLane& r, int c, float lg, float z) {
             const size_t o = (size_t)(r.R - obase) * p.C + c;
             lg_out[o] = lg;

@@ -547,9 +547,13 @@ int mcgmil_stem_forward(const mcgmil_stem_args* a, void* stream) {
     g.part = reinterpret_cast<float*>(ws + c.part);
     g.gamma = a->gamma;
     // the ResNet pool (3 x 3, stride 2, pad 1) on an even width: horizontal half in the epilogue
-    // args->flags MCGMIL_STEM_POOL_UNSPLIT, or MCGMIL_STEM_HPOOL=0 in the environment (overrides)
-    const char* hp_env = getenv("MCGMIL_STEM_HPOOL");
-    const bool unsplit = hp_env ? !strcmp(hp_env, "0") : a->flags == MCGMIL_STEM_POOL_UNSPLIT;
+    // args->flags MCGMIL_STEM_POOL_UNSPLIT, or MCGMIL_STEM_HPOOL=0|1 in the environment (overrides;
+    // read once per process)
+    static const int hp_env = [] {
+        const char* e = getenv("MCGMIL_STEM_HPOOL");
+        return e ? (strcmp(e, "0") == 0 ? 1 : 0) : -1;
+    }();
+    const bool unsplit = hp_env >= 0 ? hp_env == 1 : a->flags == MCGMIL_STEM_POOL_UNSPLIT;
     const bool hp = a->pool_kernel == 3 && a->pool_stride == 2 && a->pool_pad == 1 && G.OW % 2 == 0 && !unsplit;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (stats) hipLaunchKernelGGL(stem_prep_kernel, dim3(1), dim3(256), 0, s, g, G.KS, 1);

@@ -48,7 +48,7 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
         return out
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
     tmp = out + ".tmp"
-    objs = []
+    objs, cmds = [], []
     for src in SOURCES:     # one object per source (per-source flags), then one shared library
         obj = f"{out}.{src}.o"
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-c", "-fPIC", "-Wall", "-Werror",
@@ -56,8 +56,15 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
               [f"-D{d}" for d in defines] + [os.path.join(CSRC, src)]
         if verbose:
             print(" ".join(cmd))
-        subprocess.run(cmd, check=True)
+        cmds.append(cmd)
         objs.append(obj)
+    # the sources compile independently: in parallel (a few CPUs; each hipcc is single-threaded)
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", "0")) or (os.cpu_count() or 1), 8))
+    with ThreadPoolExecutor(jobs) as ex:
+        for r in list(ex.map(lambda c: subprocess.run(c), cmds)):
+            if r.returncode != 0:
+                raise subprocess.CalledProcessError(r.returncode, r.args)
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print(" ".join(cmd))

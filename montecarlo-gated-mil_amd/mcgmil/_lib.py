@@ -18,9 +18,12 @@ MCGMIL_BF16 = 1
 MCGMIL_U8 = 2
 MCGMIL_U16 = 3
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 # mcgmil_args.flags (include/mcgmil.h enum mcgmil_flags)
 PATH_FLAGS = {"auto": 0, "fused": 1, "two_kernel": 2}
+# mcgmil_conv_args.flags / mcgmil_stem_args.flags (include/mcgmil_features.h)
+CONV_TILE_FLAGS = {"auto": 0, "nohalo": 1, "small": 2, "big512": 3}
+STEM_POOL_UNSPLIT = 1
 GATE_FLAGS = {"auto": 0, "pipe": 1 << 2, "pp": 2 << 2, "row": 3 << 2}
 
 EXPORTED = (

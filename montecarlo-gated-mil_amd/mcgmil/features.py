@@ -141,17 +141,19 @@ def conv_input_bn(conv: nn.Conv2d, x: torch.Tensor) -> bool:
 
 
 def conv2d(conv: nn.Conv2d, x: torch.Tensor, stats: bool = False,
-           in_ab: Optional[torch.Tensor] = None, in_relu: bool = True):
+           in_ab: Optional[torch.Tensor] = None, in_relu: bool = True, flags: int = 0):
     """conv(x) for a channels-last bf16 activation (see conv_fusable) on the MFMA kernel; returns a
     channels-last bf16 tensor, or with stats=True (y, partials): the BatchNorm statistics of y
     as [parts, 3, Cout] (count, mean, M2) blocks for batchnorm_act(..., partials=...), or None
     where the layer's kernel emits none (256 x 256 tiles). With in_ab ([2, Cin] fp32 from
-    batchnorm_coefficients) the convolution reads relu?(bn(x)) instead of x (conv_input_bn)."""
+    batchnorm_coefficients) the convolution reads relu?(bn(x)) instead of x (conv_input_bn).
+    flags: mcgmil_conv_args.flags (the tile policy, MCGMIL_CONV_TILE_*; 0 = auto)."""
     if not conv_fusable(conv, x):
         raise ValueError("conv2d needs a CUDA channels-last bf16 activation, a bias-free groups=1 "
                          "convolution with 64k channels and no autograd (see conv_fusable)")
     L = _lib.load()
     a = _conv_args(conv, x)
+    a.flags = int(flags)
     if in_ab is not None:
         if in_ab.shape != (2, a.in_channels) or in_ab.dtype != torch.float32 or \
                 in_ab.device != x.device or not in_ab.is_contiguous():
@@ -249,6 +251,7 @@ def conv2d_f32(conv: nn.Conv2d, x: torch.Tensor, stats: bool = False,
                          "convolution with out_channels % 64 == 0 (conv32_fusable)")
     L = _lib.load()
     a = _conv_args(conv, x)
+    a.flags = int(flags)
     if in_ab is not None:
         if in_ab.shape != (2, a.in_channels) or in_ab.dtype != torch.float32 or \
                 in_ab.device != x.device or not in_ab.is_contiguous():
@@ -522,8 +525,9 @@ def packed_stem_weight(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
 
 
 def stem(conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool, pool: Optional[nn.MaxPool2d],
-         x: torch.Tensor) -> torch.Tensor:
-    """pool?(relu?(bn(conv(x)))) of NCHW instances (see stem_fusable) -> channels-last bf16."""
+         x: torch.Tensor, flags: int = 0) -> torch.Tensor:
+    """pool?(relu?(bn(conv(x)))) of NCHW instances (see stem_fusable) -> channels-last bf16.
+    flags: mcgmil_stem_args.flags (MCGMIL_STEM_POOL_UNSPLIT: one pooling pass; 0 = the split)."""
     if not stem_fusable(conv, bn, pool, x):
         raise ValueError("stem needs a CUDA [N, C<=4, H, W] bf16 (or autocast) input, a bias-free "
                          "stride-2 Conv2d(C, 64) with k + (pad & 1) <= 8 and OW <= 125, a "
@@ -551,6 +555,7 @@ def stem(conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool, pool: Optional[nn.MaxP
     a.x, a.w, a.y = p(xb), p(w), p(y)
     a.gamma, a.beta, a.running_mean, a.running_var = p(gamma), p(beta), p(rmean), p(rvar)
     a.eps, a.relu = float(bn.eps), int(bool(relu))
+    a.flags = int(flags)
     n = ctypes.c_size_t()
     _lib.check(L.mcgmil_stem_workspace_size(ctypes.byref(a), ctypes.byref(n)), "mcgmil_stem_workspace_size")
     ws = torch.empty(n.value, dtype=torch.uint8, device=dev)

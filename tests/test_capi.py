@@ -42,7 +42,7 @@ def test_library_targets_gfx950(hip_lib):
 
 def test_args_struct_matches_binding(hip_lib):
     from mcgmil import _lib
-    assert hip_lib.mcgmil_abi_version() == 3 == _lib.ABI_VERSION
+    assert hip_lib.mcgmil_abi_version() == 4 == _lib.ABI_VERSION
     assert hip_lib.mcgmil_conv_args_size() == ctypes.sizeof(_lib.ConvArgs)
     assert hip_lib.mcgmil_stem_args_size() == ctypes.sizeof(_lib.StemArgs)
     assert hip_lib.mcgmil_args_size() == ctypes.sizeof(_lib.Args)
@@ -72,6 +72,9 @@ def test_workspace_size_formula(hip_lib):
     rc, n = _ws(hip_lib, _args())
     assert rc == 0
     packed = (2 * 16 + 1) * 16 * 512 * 2                     # (2P+1) tiles x KS x 512 x bf16
+    # + the row-owner kernel's stream (mcgmil_rowgate.h): L/16 K steps x 2GD/32 blocks x 1 KiB,
+    # then the classifier table [4][L] bf16, after a 256-byte alignment
+    packed = ((packed + 255) // 256) * 256 + (512 // 16) * (2 * 2 * 128 // 32) * 1024 + 4 * 512 * 2
     scores = 100 * 2048 * 2 * 4
     plan = ((100 * 2048 // 16 * 4 + 255) // 256) * 256      # tile plan (int32 per 16-row tile)
     regions = 256                                            # fused region plan: int32 [B+1]
@@ -84,7 +87,7 @@ def test_workspace_size_formula(hip_lib):
     ("L", 500, -2), ("L", 4096, -2), ("D", 100, -2), ("C", 5, -2), ("C", 0, -2), ("G", 3, -1),
     ("T", 0, -1), ("num_bags", 0, -1), ("p_feat", 1.5, -1), ("p_att", -0.1, -1),
     ("h_dtype", 7, -1), ("bag_offsets", None, -1), ("total_rows", -1, -1),
-    ("flags", 3, -1), ("flags", 3 << 2, -1), ("flags", 16, -1), ("reserved", 1, -1),
+    ("flags", 3, -1), ("flags", 16, -1), ("reserved", 1, -1),
 ])
 def test_validation_errors(hip_lib, field, value, code):
     rc, _ = _ws(hip_lib, _args(**{field: value}))
@@ -107,9 +110,8 @@ def test_path_flags_select_the_launch(hip_lib, monkeypatch):
     """mcgmil_args.flags picks the launch mcgmil_gate_softmax_pool makes (host logic, no launch):
     auto = fused only for bf16 batches of equal-size bags with >= 16,384 regions; FUSED whenever
     it applies; TWO_KERNEL never; MCGMIL_GATE_PP keeps bf16 heads off the fused (pipe) tile code;
-    MCGMIL_FUSED in the environment overrides the flags."""
+    MCGMIL_GATE_ROW takes the row-gate fused launch."""
     from mcgmil import _lib
-    monkeypatch.delenv("MCGMIL_FUSED", raising=False)
     F, G = _lib.PATH_FLAGS, _lib.GATE_FLAGS
     small = dict(num_bags=16, total_rows=16 * 2048, uniform_bag_rows=2048)
     big = dict(num_bags=512, total_rows=512 * 2048, uniform_bag_rows=2048)
@@ -119,14 +121,40 @@ def test_path_flags_select_the_launch(hip_lib, monkeypatch):
     assert _regions(hip_lib, _args(flags=F["two_kernel"], **big)) == 0
     assert _regions(hip_lib, _args(flags=F["fused"] | G["pp"], **small)) == 0
     assert _regions(hip_lib, _args(flags=F["fused"] | G["pipe"], **small)) == 16 * 50
+    assert _regions(hip_lib, _args(flags=F["fused"] | G["row"], **small)) == 16 * 50
     assert _regions(hip_lib, _args(flags=F["fused"], h_dtype=_lib.MCGMIL_F32, **small)) == 16 * 50
     assert _regions(hip_lib, _args(h_dtype=_lib.MCGMIL_F32, **big)) == 0      # fp32: auto stays off
-    monkeypatch.setenv("MCGMIL_FUSED", "1")
-    assert _regions(hip_lib, _args(flags=F["two_kernel"], **small)) == 16 * 50
-    monkeypatch.setenv("MCGMIL_FUSED", "0")
-    assert _regions(hip_lib, _args(flags=F["fused"], **big)) == 0
-    monkeypatch.setenv("MCGMIL_FUSED", "auto")
-    assert _regions(hip_lib, _args(flags=F["fused"], **small)) == 0
+
+
+_ENV_PROBE = r"""
+import ctypes, sys
+sys.path[:0] = [{repo!r}, {pkg!r}]
+import test_capi as t
+from mcgmil import _lib
+lib = _lib.load()
+F = _lib.PATH_FLAGS
+small = dict(num_bags=16, total_rows=16 * 2048, uniform_bag_rows=2048)
+big = dict(num_bags=512, total_rows=512 * 2048, uniform_bag_rows=2048)
+print(t._regions(lib, t._args(flags=F["two_kernel"], **small)), t._regions(lib, t._args(flags=F["fused"], **big)),
+      t._regions(lib, t._args(flags=F["fused"], **small)))
+"""
+
+
+@pytest.mark.parametrize("env,want", [("1", [16 * 50, 512 * 50, 16 * 50]), ("0", [0, 0, 0]),
+                                      ("auto", [0, 512 * 50, 0])])
+def test_fused_environment_override(hip_lib, env, want):
+    """MCGMIL_FUSED in the environment overrides the flags; it is read once per process, so each
+    setting runs in a fresh interpreter (host logic, no launch)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    code = _ENV_PROBE.format(repo=here, pkg=os.path.join(repo, "montecarlo-gated-mil_amd"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, MCGMIL_FUSED=env))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert [int(v) for v in r.stdout.split()[-3:]] == want
 
 
 def test_forward_rejects_missing_workspace(hip_lib):

@@ -8,8 +8,15 @@ mcgmil_fused.hip compiled with the library's own flags (mcgmil/_build.py; hipcc 
 * so does the launch bench.py times (gate_fused_kernel, bf16 separate heads; mcgmil_fused.hip with
   its own flags), and it has no packed-fp32 VALU either;
 * the halo convolutions of the config-5 backbone (conv3x3c64_kernel, conv3x3_halo_kernel; every
-  STATS / input-BN instantiation) have no scratch: they run one 8-wave workgroup per CU at the
-  register limit, and a spill would put scratch traffic into the tap loop.
+  STATS / input-BN instantiation) have no scratch and fit 256 registers: they run one 8-wave
+  workgroup per CU (two waves per SIMD), and a spill would put scratch traffic into the tap loop;
+* every row-owner gate kernel (rowgate_scores_kernel, rowgate_fused_kernel; mcgmil_rowgate.h) has
+  no scratch: the LDS-DMA instantiations read the weight ring with inline-asm ds_reads whose
+  destination registers the compiler cannot see in flight, so a spill or copy of one of them before
+  its wait would read stale data (the register-staged instantiations are compiler-visible);
+* the stem convolution (stem_conv_kernel) drains its LDS-DMA staging (s_waitcnt vmcnt(0)) right
+  before every barrier that publishes a staged tile: its epilogue's LDS accesses are inline asm the
+  compiler's wait-count pass cannot see, so nothing else would order them after the DMA.
 """
 import os
 import re
@@ -89,6 +96,22 @@ def test_fused_kernel_fits_without_spills(fused_asm):
     assert kernel_meta(fused_asm, FUSED, "num_vgpr") + kernel_meta(fused_asm, FUSED, "num_agpr") <= 256
 
 
+def _rowgate_syms(text, kind):
+    return set(re.findall(rf"\.set (_ZN6mcgmil\d+rowgate_{kind}_kernel\w*)\.private_seg_size", text))
+
+
+def test_rowgate_kernels_fit_without_spills(device_asm, fused_asm):
+    scores, fused = _rowgate_syms(device_asm, "scores"), _rowgate_syms(fused_asm, "fused")
+    # G in {1, 2} x MAXC in {2, 4} x {Philox, replayed masks}; the fused kernel makes its own masks
+    assert len(scores) == 8 and len(fused) == 4, (scores, fused)
+    assert any(s.endswith("Lb1EEEvNS_10GateParamsE") for s in scores | fused), "no LDS-DMA instantiation"
+    for text, syms in ((device_asm, scores), (fused_asm, fused)):
+        for sym in syms:
+            assert kernel_meta(text, sym, "private_seg_size") == 0, sym
+            # one wave per SIMD: the whole unified register file
+            assert kernel_meta(text, sym, "num_vgpr") + kernel_meta(text, sym, "num_agpr") <= 512, sym
+
+
 @pytest.fixture(scope="module")
 def conv_asm(tmp_path_factory):
     return _asm(tmp_path_factory, "mcgmil_conv.hip")
@@ -100,4 +123,38 @@ def test_halo_conv_kernels_fit_without_spills(conv_asm):
     assert len(syms) == 8, syms
     for sym in syms:
         assert kernel_meta(conv_asm, sym, "private_seg_size") == 0, sym
-        assert kernel_meta(conv_asm, sym, "num_vgpr") + kernel_meta(conv_asm, sym, "num_agpr") <= 512, sym
+        # 512-thread workgroups, one per CU: two waves per SIMD, 256 registers each
+        assert kernel_meta(conv_asm, sym, "num_vgpr") + kernel_meta(conv_asm, sym, "num_agpr") <= 256, sym
+
+
+@pytest.fixture(scope="module")
+def stem_asm(tmp_path_factory):
+    return _asm(tmp_path_factory, "mcgmil_stem.hip")
+
+
+def _barrier_predecessors(text, sym):
+    i = text.index(sym + ":")
+    j = text.index(".Lfunc_end", i)
+    lines = [x.split(";")[0].strip() for x in text[i:j].split("\n")]
+    out = []
+    for k, x in enumerate(lines):
+        if x.startswith("s_barrier"):
+            q = k - 1
+            while q > 0 and (not lines[q] or lines[q].startswith(".")):
+                q -= 1
+            out.append(lines[q])
+    return out
+
+
+def test_stem_barriers_drain_the_staging_dma(stem_asm):
+    syms = sorted(set(re.findall(r"^(_ZN12_GLOBAL__N_1\d+stem_conv_kernelILi\dELb([01])ELb[01]EEEvNS_8StemGeomE):",
+                                 stem_asm, flags=re.M)))
+    assert len(syms) == 32, len(syms)
+    for sym, stats in syms:
+        prev = _barrier_predecessors(stem_asm, sym)
+        # the prologue's and the tile loop's barriers; STATS kernels end with one more barrier for
+        # the statistics reduction, after the last DMA has been waited for
+        staged = prev[:-1] if stats == "1" else prev
+        assert len(staged) >= 2, (sym, prev)
+        for x in staged:
+            assert x.startswith("s_waitcnt") and "vmcnt(0)" in x, (sym, prev)

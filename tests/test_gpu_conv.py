@@ -39,8 +39,10 @@ SHAPES = [
     (4, 128, 25, 20, 128, 3, 1, 1),
     (2, 192, 17, 30, 256, 3, 1, 1),
     (1, 128, 6, 80, 128, 3, 1, 1),
-    # 1x1 / stride 2 streaming kernel: layer 3's shape at odd sizes (pixels not a multiple of the
-    # 16-pixel fragment), 192 output channels (6 waves per pixel stream), a single image
+    # 1x1 / stride 2: from 64 input channels the streaming kernel (conv1x1_kernel; odd pixel
+    # counts, 192 output channels = 6 waves per pixel stream); from 128 / 256 channels (layer 3's and
+    # 4's shapes at odd sizes, a single image) the LDS-DMA tiles (make_plan sends only Cin == 64 to
+    # the streaming kernel)
     (3, 128, 13, 11, 256, 1, 2, 0),
     (2, 64, 9, 7, 192, 1, 2, 0),
     (1, 256, 14, 14, 512, 1, 2, 0),
@@ -74,6 +76,35 @@ def test_conv2d_matches_fp64(cuda, shape):
     assert y.shape == ref.shape
     err = (y.double() - ref).abs()
     assert torch.all(err <= 2.0 ** -8 * ref.abs() + 1e-5 * mag), float((err / (ref.abs() + 1e-30)).max())
+
+
+TILE_SHAPES = [(3, 64, 56, 56, 64, 3, 1, 1), (3, 128, 28, 28, 128, 3, 1, 1), (2, 256, 14, 14, 512, 3, 2, 1),
+               (2, 64, 9, 7, 192, 1, 2, 0)]
+
+
+@pytest.mark.parametrize("shape", TILE_SHAPES)
+def test_conv2d_tile_policy_flags(cuda, shape):
+    """mcgmil_conv_args.flags (MCGMIL_CONV_TILE_*: auto, no halo / streaming kernels, 256 x 128 for
+    256 x 256 tiles, 512 x 128 on 128-channel layers) selects the kernel without the environment;
+    every policy is within the fp64 bound and repeatable."""
+    from mcgmil import _lib
+    from mcgmil.features import conv2d
+    N, Cin, H, W, Cout, k, s, p = shape
+    conv = _layer(Cin, Cout, k, s, p, cuda, Cin + 2 * Cout + k)
+    g = torch.Generator(device=cuda).manual_seed(N * W + H)
+    x = torch.randn(N, Cin, H, W, device=cuda, generator=g).relu_().bfloat16()
+    x = x.contiguous(memory_format=torch.channels_last)
+    wb = conv.weight.detach().bfloat16().double()
+    with torch.no_grad():
+        ref = F.conv2d(x.double(), wb, None, s, p)
+        mag = F.conv2d(x.double().abs(), wb.abs(), None, s, p)
+    for name, flag in _lib.CONV_TILE_FLAGS.items():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            y = conv2d(conv, x, flags=flag)
+            y2 = conv2d(conv, x, flags=flag)
+        assert torch.equal(y, y2), name
+        err = (y.double() - ref).abs()
+        assert torch.all(err <= 2.0 ** -8 * ref.abs() + 1e-5 * mag), name
 
 
 def test_conv2d_bf16_weights_and_repack(cuda):
@@ -151,6 +182,10 @@ STATS_SHAPES = [
     (2, 192, 17, 30, 256, 3, 1, 1, 2.0),
     (3, 128, 13, 11, 256, 1, 2, 0, 2.0),
     (2, 64, 28, 28, 128, 1, 2, 0, 0.0),
+    # streaming 1x1 kernel with more pixel streams than fragments: M = 9 pixels (1 fragment), 6
+    # channel blocks, the stream count rounded up to 2 -- an empty stream whose statistics rows have
+    # count 0 and must merge away in the BN finalize
+    (1, 64, 6, 6, 192, 1, 2, 0, 0.0),
 ]
 
 

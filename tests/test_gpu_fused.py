@@ -6,10 +6,9 @@ Both paths run the same tile code and the same softmax_group, so every output mu
 equal. The cases cover the fused kernel's region shapes: several t-groups per region (small N),
 one t-group per region (N = 2048 at cap 4096), bags larger than the LDS cap (logits through the
 global workspace, incl. > 4,096 instances: the streaming softmax), empty bags (Y = 0), ragged
-batches (the device region plan) and uniform ones (arithmetic region map), C = 1, 2, 4."""
-import contextlib
-import os
-
+batches (the device region plan) and uniform ones (arithmetic region map), C = 1, 2, 4.
+The launch is chosen through mcgmil_args.flags (path=, gate=): the MCGMIL_FUSED / MCGMIL_GATE
+overrides are read once per process (tests/test_capi.py runs them in a subprocess)."""
 import numpy as np
 import pytest
 import torch
@@ -21,29 +20,16 @@ from mcgmil import synthetic
 pytestmark = pytest.mark.gpu
 
 
-@contextlib.contextmanager
-def fused(mode):
-    old = os.environ.get("MCGMIL_FUSED")
-    os.environ["MCGMIL_FUSED"] = mode
-    try:
-        yield
-    finally:
-        if old is None:
-            del os.environ["MCGMIL_FUSED"]
-        else:
-            os.environ["MCGMIL_FUSED"] = old
-
-
 def head_on(arrays, dev):
     from mcgmil.ops import HeadTensors
     return HeadTensors(*[torch.from_numpy(np.ascontiguousarray(arrays[k])).to(dev)
                          for k in HeadTensors._fields])
 
 
-def regions(H, offs, head, T):
+def regions(H, offs, head, T, path="auto", gate="auto"):
     import ctypes
     from mcgmil import _lib, ops
-    a = ops.make_args(H, offs, head, T, head.C, head.G, head.D, 0.1, 0.1, seed=1)
+    a = ops.make_args(H, offs, head, T, head.C, head.G, head.D, 0.1, 0.1, seed=1, path=path, gate=gate)
     n = ctypes.c_size_t()
     _lib.check(_lib.load().mcgmil_workspace_size(ctypes.byref(a), ctypes.byref(n)), "ws")
     ws = torch.empty(max(n.value, 1), dtype=torch.uint8, device=H.device)
@@ -79,12 +65,10 @@ def test_fused_equals_two_kernel_path(cuda, case):
     offs = ops.bag_offsets_tensor(sizes, cuda)
     ids = torch.tensor([7 * b + 3 for b in range(len(sizes))], dtype=torch.int32, device=cuda)
     kw = dict(p_feat=0.1, p_att=0.1, seed=1234, bag_ids=ids, return_stats=True)
-    with fused("0"):
-        assert regions(H, offs, head, T) == 0
-        ref = ops.mcdo_forward(H, offs, head, T, **kw)
-    with fused("1"):
-        nreg = regions(H, offs, head, T)
-        out = ops.mcdo_forward(H, offs, head, T, **kw)
+    assert regions(H, offs, head, T, path="two_kernel") == 0
+    ref = ops.mcdo_forward(H, offs, head, T, path="two_kernel", **kw)
+    nreg = regions(H, offs, head, T, path="fused")
+    out = ops.mcdo_forward(H, offs, head, T, path="fused", **kw)
     torch.cuda.synchronize()
     if dtype == torch.bfloat16 and (shared or C == 1):
         assert nreg == 0           # bf16 heads of <= 8 gate tile pairs run gate_pp_kernel: not fused
@@ -99,10 +83,9 @@ def test_fused_equals_two_kernel_path(cuda, case):
 
 
 def test_fused_auto_policy(cuda):
-    """MCGMIL_FUSED=auto (also the default, unset) takes the fused launch only for bf16 batches of
-    equal-size bags with >= 16,384 regions: 16 bags of N=2048, T=100 (800 regions of two t-groups)
-    do not, 512 bags (25,600, the bench's step) do, ragged or fp32 batches do not. MCGMIL_FUSED=0:
-    never."""
+    """path="auto" (the default) takes the fused launch only for bf16 batches of equal-size bags
+    with >= 16,384 regions: 16 bags of N=2048, T=100 (800 regions of two t-groups) do not, 512 bags
+    (25,600, the bench's step) do, ragged or fp32 batches do not. path="two_kernel": never."""
     from mcgmil import ops
     sd = synthetic.head_state_dict(0, C=2, shared=False)
     head = head_on(synthetic.head_arrays(sd, 2, False), cuda)
@@ -110,31 +93,18 @@ def test_fused_auto_policy(cuda):
     small_offs = ops.bag_offsets_tensor([2048] * 16, cuda)
     big = torch.zeros(512 * 2048, 512, device=cuda, dtype=torch.bfloat16)
     big_offs = ops.bag_offsets_tensor([2048] * 512, cuda)
-    with fused("auto"):
-        assert regions(small, small_offs, head, 100) == 0
-        assert regions(big, big_offs, head, 100) == 512 * 50
-    old = os.environ.pop("MCGMIL_FUSED", None)
-    try:
-        assert regions(small, small_offs, head, 100) == 0
-        assert regions(big, big_offs, head, 100) == 512 * 50
-    finally:
-        if old is not None:
-            os.environ["MCGMIL_FUSED"] = old
-    with fused("0"):
-        assert regions(big, big_offs, head, 100) == 0
+    assert regions(small, small_offs, head, 100) == 0
+    assert regions(big, big_offs, head, 100) == 512 * 50
+    assert regions(big, big_offs, head, 100, path="two_kernel") == 0
     # ragged batches (config 4) stay on the two-kernel path under auto, however many regions
     ragged_offs = ops.bag_offsets_tensor([2047, 2049] * 256, cuda)
-    with fused("auto"):
-        assert regions(big, ragged_offs, head, 100) == 0
-    with fused("1"):
-        assert regions(big, ragged_offs, head, 100) > 16384
+    assert regions(big, ragged_offs, head, 100) == 0
+    assert regions(big, ragged_offs, head, 100, path="fused") > 16384
     # fp32 stays on the two-kernel path under auto (the fused fp32 tile loop spills: 13-18% slower)
     big32 = torch.zeros(1280 * 512, 512, device=cuda, dtype=torch.float32)   # 1280 bags x 13 regions
     offs32 = ops.bag_offsets_tensor([512] * 1280, cuda)
-    with fused("auto"):
-        assert regions(big32, offs32, head, 100) == 0
-    with fused("1"):
-        assert regions(big32, offs32, head, 100) == 1280 * 13
+    assert regions(big32, offs32, head, 100) == 0
+    assert regions(big32, offs32, head, 100, path="fused") == 1280 * 13
 
 
 from test_gpu_parity import BF16_CASES, FP32_CASES, TOL32, TOL_BF16_IN, compare, run  # noqa: E402
@@ -147,8 +117,7 @@ def test_fused_matches_reference_goldens(cuda, name):
     run the two-kernel path here)."""
     case = Case(name)
     bf16 = name in BF16_CASES
-    with fused("1"):
-        out = run(case, cuda, torch.bfloat16 if bf16 else torch.float32)
+    out = run(case, cuda, torch.bfloat16 if bf16 else torch.float32, path="fused")
     compare(case, out, TOL_BF16_IN if bf16 else TOL32)
 
 
@@ -160,9 +129,9 @@ def test_fused_config3_bag_vs_oracle(cuda):
     sd = synthetic.head_state_dict(seed, C=2, shared=False)
     Hn = synthetic.bf16_round(synthetic.bag_features(seed + 1, N))
     head = head_on(synthetic.head_arrays(sd, 2, False), cuda)
-    with fused("1"):
-        out = ops.mcdo_forward(torch.from_numpy(Hn).to(cuda).bfloat16(), ops.bag_offsets_tensor([N], cuda),
-                               head, T, p_feat=0.1, p_att=0.1, seed=seed, bag_id_base=9, return_stats=True)
+    out = ops.mcdo_forward(torch.from_numpy(Hn).to(cuda).bfloat16(), ops.bag_offsets_tensor([N], cuda),
+                           head, T, p_feat=0.1, p_att=0.1, seed=seed, bag_id_base=9, return_stats=True,
+                           path="fused")
     torch.cuda.synchronize()
     kF, kA = mcdo_ref.masks_for_bag(seed, 9, T, N, 512, 2, 0.1, 0.1)
     Yr, Ar = mcdo_ref.mc_inference(Hn, mcdo_ref.HeadParams(synthetic.head_arrays(
@@ -268,9 +237,9 @@ def test_fused_bench_step_shape(cuda):
         _check_vs_oracle(out, b, b * N, N, T, Yr, Ar)
 
 
-def test_path_flag_matches_environment_override(cuda):
-    """mcgmil_args.flags and the MCGMIL_FUSED override select the same launches (counted by
-    fused_regions) and give bitwise the same outputs."""
+def test_path_and_gate_flags_agree(cuda):
+    """mcgmil_args.flags: the fused launch, the two-kernel launch and the two-kernel launch with
+    the gate kernel forced (gate="pipe") give bitwise the same outputs; an unknown path raises."""
     from mcgmil import ops
     sizes = [300] * 8
     sd = synthetic.head_state_dict(3, C=2, shared=False)
@@ -280,13 +249,82 @@ def test_path_flag_matches_environment_override(cuda):
     offs = ops.bag_offsets_tensor(sizes, cuda)
     kw = dict(p_feat=0.1, p_att=0.1, seed=9, return_stats=True)
     a = ops.mcdo_forward(H, offs, head, 30, path="fused", **kw)
-    with fused("1"):
-        b = ops.mcdo_forward(H, offs, head, 30, path="two_kernel", **kw)   # env wins: fused
+    b = ops.mcdo_forward(H, offs, head, 30, path="two_kernel", **kw)
     c = ops.mcdo_forward(H, offs, head, 30, path="two_kernel", gate="pipe", **kw)
     for k in a:
         assert torch.equal(a[k], b[k]) and torch.equal(a[k], c[k]), k
     with pytest.raises(ValueError):
         ops.mcdo_forward(H, offs, head, 30, path="bogus", **kw)
+
+
+# ------------------------------------------------------------------ the row-owner gate kernel
+ROW_CASES = [
+    # name, sizes, T, C, shared, p_feat, p_att
+    ("sep_uniform", [2048] * 2, 6, 2, False, 0.1, 0.1),
+    ("shared_uniform", [2048] * 2, 6, 2, True, 0.1, 0.1),
+    ("sep_ragged", [1, 37, 200, 513, 0, 130, 4100], 5, 2, False, 0.1, 0.5),
+    ("shared_ragged_c3", [129, 3, 640, 5000], 7, 3, True, 0.37, 0.1),
+    ("sep_c4", [300, 77], 4, 4, False, 0.1, 0.1),
+    ("sep_c1_p0", [300], 3, 1, False, 0.0, 0.0),
+    ("sep_p1", [100, 64], 2, 2, False, 1.0, 1.0),
+]
+
+
+@pytest.mark.parametrize("case", ROW_CASES, ids=[c[0] for c in ROW_CASES])
+def test_row_gate_fused_two_kernel_oracle(cuda, case):
+    """gate="row" (MCGMIL_GATE_ROW: rowgate_scores_kernel / rowgate_fused_kernel, mcgmil_rowgate.h):
+    fused and two-kernel launches bitwise equal, and every non-empty bag against the reference
+    restatement (mcdo_ref, model.py:280-316) with the kernel's own masks on the same bf16 operands."""
+    from mcgmil import ops
+    from test_gpu_parity import TOL_BF16_IN
+    name, sizes, T, C, shared, p_f, p_a = case
+    L, seed = 512, 808
+    sd = synthetic.head_state_dict(seed, L=L, C=C, shared=shared)
+    Hs = [synthetic.bf16_round(synthetic.bag_features(seed + 10 + b, n, L)) for b, n in enumerate(sizes)]
+    head = head_on(synthetic.head_arrays(sd, C, shared), cuda)
+    H = torch.from_numpy(np.concatenate(Hs)).to(cuda).bfloat16().contiguous()
+    offs = ops.bag_offsets_tensor(sizes, cuda)
+    kw = dict(p_feat=p_f, p_att=p_a, seed=seed, bag_id_base=3, return_stats=True, gate="row")
+    # the row kernel runs one or two gates; four separate heads fall back to the tile kernels
+    assert (regions(H, offs, head, T, path="fused", gate="row") > 0) == (head.G <= 2)
+    two = ops.mcdo_forward(H, offs, head, T, path="two_kernel", **kw)
+    fz = ops.mcdo_forward(H, offs, head, T, path="fused", **kw)
+    torch.cuda.synchronize()
+    for k in two:
+        assert torch.equal(torch.nan_to_num(fz[k], nan=7.0), torch.nan_to_num(two[k], nan=7.0)), k
+    prm = mcdo_ref.HeadParams(synthetic.head_arrays(synthetic.round_state_dict_bf16(sd), C, shared))
+    Y = two["Y"].cpu().numpy()
+    A = ops.split_bags(two["A"].cpu(), sizes, T * C)
+    for b, n in enumerate(sizes):
+        if n == 0:
+            assert np.all(Y[b] == 0)
+            continue
+        kF, kA = mcdo_ref.masks_for_bag(seed, 3 + b, T, n, L, C, p_f, p_a)
+        Yr, Ar = mcdo_ref.mc_inference(Hs[b], prm, kF, kA, p_f, p_a)
+        np.testing.assert_allclose(Y[b], Yr[:, 0].numpy(), rtol=0, atol=TOL_BF16_IN["Y"])
+        Ar = Ar[:, 0].numpy()
+        assert np.abs(A[b].numpy().reshape(T, C, n) - Ar).max() <= TOL_BF16_IN["A"] * max(np.abs(Ar).max(), 1e-30)
+
+
+@pytest.mark.parametrize("shared", [False, True])
+def test_row_gate_replayed_masks_equal_philox(cuda, shared):
+    """The row kernel with the masks handed in (keep_feat / keep_att, the replay instantiations:
+    register-staged weights for C = 4 separate heads, LDS-DMA otherwise) is bitwise its own Philox run."""
+    from mcgmil import ops
+    for C in (2, 4):
+        sizes, T = [700, 33], 4
+        sd = synthetic.head_state_dict(3, L=512, C=C, shared=shared)
+        head = head_on(synthetic.head_arrays(sd, C, shared), cuda)
+        H = torch.from_numpy(np.concatenate([synthetic.bag_features(9 + b, n, 512) for b, n in enumerate(sizes)])) \
+            .to(cuda).bfloat16().contiguous()
+        offs = ops.bag_offsets_tensor(sizes, cuda)
+        R = sum(sizes)
+        kf = ops.feature_keep(offs, R, T, 512, 0.1, 11)
+        ka = ops.attention_keep(offs, R, T, C, 0.1, 11)
+        kw = dict(p_feat=0.1, p_att=0.1, seed=11, path="two_kernel", gate="row")
+        a = ops.mcdo_forward(H, offs, head, T, **kw)
+        b = ops.mcdo_forward(H, offs, head, T, keep_feat=kf, keep_att=ka, **kw)
+        assert torch.equal(a["Y"], b["Y"]) and torch.equal(a["A"], b["A"]), C
 
 
 def _random_cases(n=12, seed=2024):

@@ -35,7 +35,7 @@ def head_on(arrays, dev):
                          for k in HeadTensors._fields])
 
 
-def run(case, dev, dtype, replay=False, H=None):
+def run(case, dev, dtype, replay=False, H=None, **launch):
     from mcgmil import ops
     Hn, _, arrays = case.inputs()
     Hn = Hn if H is None else H
@@ -48,7 +48,7 @@ def run(case, dev, dtype, replay=False, H=None):
         kw["keep_att"] = torch.from_numpy(kA.astype(np.uint8).reshape(-1)).to(dev)
     out = ops.mcdo_forward(Ht, offs, head_on(arrays, dev), case.T, p_feat=case.p_f,
                            p_att=case.p_a, seed=case.mask_seed, bag_id_base=case.bag_ctr,
-                           return_stats=True, **kw)
+                           return_stats=True, **kw, **launch)
     torch.cuda.synchronize()
     return {k: v.cpu().numpy() for k, v in out.items()}
 

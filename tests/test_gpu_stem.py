@@ -159,8 +159,9 @@ def test_stem_fusable_gates(cuda):
 def test_stem_row_pooled_epilogue_bitwise(cuda, shape, running):
     """The 3 x 3 / 2 pool split into a horizontal half in the convolution epilogue and a vertical
     pass (negated channels where gamma < 0, zero gammas included) equals the unsplit pooling pass
-    bit for bit (MCGMIL_STEM_HPOOL=0); full and partial 16-pixel fragments."""
-    import os
+    bit for bit (mcgmil_stem_args.flags = MCGMIL_STEM_POOL_UNSPLIT); full and partial 16-pixel
+    fragments."""
+    from mcgmil import _lib
     from mcgmil.features import stem
     N, C, H, W = shape
     conv, bn = _stem_layers(C, 7, 3, cuda, H + W, running)
@@ -171,11 +172,7 @@ def test_stem_row_pooled_epilogue_bitwise(cuda, shape, running):
     g = torch.Generator(device=cuda).manual_seed(N + H)
     x = (torch.randn(N, C, H, W, device=cuda, generator=g) * 1.5).bfloat16()
     outs = {}
-    for flag in ("1", "0"):
-        os.environ["MCGMIL_STEM_HPOOL"] = flag
-        try:
-            with torch.no_grad():
-                outs[flag] = stem(conv, bn, True, pool, x)
-        finally:
-            os.environ.pop("MCGMIL_STEM_HPOOL", None)
-    assert torch.equal(outs["1"], outs["0"])
+    for flag in (0, _lib.STEM_POOL_UNSPLIT):
+        with torch.no_grad():
+            outs[flag] = stem(conv, bn, True, pool, x, flags=flag)
+    assert torch.equal(outs[0], outs[_lib.STEM_POOL_UNSPLIT])
