@@ -33,6 +33,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "bags/sec × MCDO-samples (T=100) at N=2048,d=512; 1/2/4/8-GPU + %HBM roofline"
 PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}   # MI355X dense MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+MAX_CLOCK_MHZ = 2400.0                          # the clock the spec peaks are quoted at
 
 
 def flops_per_bag(N, T, L, D, C, G):
@@ -69,9 +70,31 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def host_cores():
+    """The CPUs this process may run on: its affinity mask, capped by the cgroup (v2 cpu.max or
+    v1 cfs quota) CPU quota when there is one. Returns (count, provenance dict)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    n = aff if quota is None else max(1, min(aff, int(quota)))
+    return n, {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "os_cpu_count": os.cpu_count()}
+
+
 def cpu_baseline(N, T, L, D, C, shared, budget_s):
-    """The reference CPU path (torch op sequence incl. dropout RNG), bounded sample, on all the
-    host threads torch uses and on one thread (BASELINE.md's plan)."""
+    """The reference CPU path (torch op sequence incl. dropout RNG), bounded sample, on every CPU
+    this process may use (affinity, capped by the cgroup quota) and on one thread (BASELINE.md's
+    plan)."""
     from oracle import mcdo_ref
     from mcgmil import synthetic
     arrays = synthetic.head_arrays(synthetic.head_state_dict(0, L=L, D=D, C=C, shared=shared), C, shared)
@@ -89,16 +112,18 @@ def cpu_baseline(N, T, L, D, C, shared, budget_s):
                 if el >= budget or n >= max_bags:
                     return n, el
 
-    threads = torch.get_num_threads()
-    n, el = timed(budget_s, 50)
-    torch.set_num_threads(1)
+    before = torch.get_num_threads()
+    threads, prov = host_cores()
+    torch.set_num_threads(threads)
     try:
+        n, el = timed(budget_s, 50)
+        torch.set_num_threads(1)
         n1, el1 = timed(budget_s / 3, 10)
     finally:
-        torch.set_num_threads(threads)
+        torch.set_num_threads(before)
     model = cpu_model()
     return {"value": n * T / el, "unit": "bag-samples/s", "cores": threads, "kind": "port",
-            "cpu_model": model,
+            "cpu_model": model, "cores_provenance": prov,
             "single_thread": {"value": n1 * T / el1, "unit": "bag-samples/s", "cores": 1,
                               "ms_per_bag": el1 * 1e3 / n1, "bags": n1},
             "sample": f"{n} bags of N={N}, T={T}, fp32, {'shared' if shared else 'separate'} "
@@ -214,8 +239,10 @@ def main():
 
     # the reference's precision at the metric's shape (model.py:280-316 computes in fp32), and the
     # one-bag-per-call caller (infer.py:187-191): N = 1 only, after the headline's timed steps
-    fp32_line = single = None
+    fp32_line = single = shared_line = None
     if world == 1 and args.workload == "cfg3" and not args.no_secondary:
+        if not args.shared:
+            shared_line = shared_secondary(args, dev)
         fp32_line = fp32_secondary(args, dev)
         single = single_bag_line(args, dev, quiet=True)
 
@@ -247,7 +274,8 @@ def main():
                          # what the HIP events bracket: the whole path (gate scores + softmax +
                          # pooling) when fused, the gate GEMM kernel alone otherwise
                          "timed_path": "fused: gate+softmax+pooling" if fused else "two-kernel: gate only",
-                         "kernel_ms": gate_ms, "algorithmic_tflop_per_launch": F / 1e12},
+                         "kernel_ms": gate_ms, "algorithmic_tflop_per_launch": F / 1e12,
+                         **at_clock(achieved, PEAK_TFLOPS[args.dtype], r["clock"])},
             "roofline_hbm": {"achieved": hbm_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": hbm_gbs / PEAK_HBM_GBS,
                              "algorithmic_bytes_per_launch": hbm_bytes},
@@ -258,6 +286,7 @@ def main():
                 "value": total_bag_samples / r["cold"][0], "ms_per_step": r["cold"][0] * 1e3 / args.steps,
                 "kernel_ms": r["cold"][1],
                 "frac": F / (r["cold"][1] * 1e-3) / 1e12 / PEAK_TFLOPS[args.dtype]},
+            "shared_heads": shared_line,
             "fp32_reference_precision": fp32_line,
             "single_bag": single,
             "cpu_baseline": cpu,
@@ -386,8 +415,55 @@ def measure_batch(sizes, ids, T, dtype, shared, dev, world, steps, warmup, busy_
     torch.cuda.synchronize()
     busy = time.perf_counter() - t_busy
     el, gate_ms = timed_pass()
+    # the clock the gate launch runs at: one more (untimed) step right after the timed ones, its
+    # workgroups stamping s_memtime / s_memrealtime at start and end (MCGMIL_CLOCK_PROBE)
+    rec = ops.clock_record(dev)
+    a.debug, a.flags = ctypes.c_void_p(rec.data_ptr()), a.flags | _lib.CLOCK_PROBE
+    step()
+    torch.cuda.synchronize()
+    a.debug, a.flags = None, a.flags & ~_lib.CLOCK_PROBE
+    clock = ops.clock_mhz(rec)
+    if world > 1 and clock is not None:
+        t = torch.tensor([clock["median"]], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)     # the slowest rank's clock
+        clock["median_min_over_ranks"] = float(t)
     return {"el": el, "gate_ms": gate_ms, "fused": fused, "regions": regions.value,
-            "packed_bytes": packed.numel(), "busy_s": busy, "busy_extra_steps": extra, "cold": cold}
+            "packed_bytes": packed.numel(), "busy_s": busy, "busy_extra_steps": extra, "cold": cold,
+            "clock": clock}
+
+
+def at_clock(achieved, peak, clock):
+    """The roofline's clock keys: the shader clock the launch ran at and the fraction of the peak
+    scaled to that clock (the spec peak assumes MAX_CLOCK_MHZ)."""
+    if clock is None:
+        return {"clock_mhz": None, "frac_at_clock": None}
+    return {"clock_mhz": round(clock["median"], 1), "clock_mhz_p10_p90": [round(clock["p10"], 1), round(clock["p90"], 1)],
+            "frac_at_clock": achieved / (peak * clock["median"] / MAX_CLOCK_MHZ),
+            "clock_source": f"in-kernel s_memtime/s_memrealtime x 100 MHz, median of {clock['workgroups']} "
+                            f"workgroups of one probed launch right after the timed steps"}
+
+
+def shared_secondary(args, dev, steps=10, warmup=3):
+    """The reference constructor's default head layout (shared_attention=True, model.py:144,
+    182-184: one gate pair feeds every class) on the headline's workload: --bags bags of N=--n,
+    T=--T, bf16, its own algorithmic FLOPs (G = 1) against the bf16 peak."""
+    N, T, L, D, C = args.n, args.T, 512, 128, 2
+    bags = args.bags
+    r = measure_batch([N] * bags, list(range(bags)), T, args.dtype, True, dev, 1, steps, warmup)
+    F = bags * flops_per_bag(N, T, L, D, C, 1)
+    ach = F / (r["gate_ms"] * 1e-3) / 1e12
+    return {"metric": "bag-samples/s, shared attention (the reference constructor's default)",
+            "value": bags * T * steps / r["el"], "unit": "bag-samples/s", "dtype": args.dtype,
+            "steps": steps, "warmup": warmup, "ms_per_step": r["el"] * 1e3 / steps,
+            "config": f"{bags} bags of N={N}, d={L}, D={D}, C={C}, T={T}, shared attention, {args.dtype}",
+            "gflop_per_bag": flops_per_bag(N, T, L, D, C, 1) / 1e9,
+            "roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_TFLOPS[args.dtype], "unit": "TFLOP/s",
+                         "frac": ach / PEAK_TFLOPS[args.dtype], "kernel_ms": r["gate_ms"],
+                         "kernel": (f"fused launch ({r['regions']} regions)" if r["fused"]
+                                    else "gate kernel (two-kernel path)"),
+                         "timed_path": "fused: gate+softmax+pooling" if r["fused"] else "two-kernel: gate only",
+                         "algorithmic_tflop_per_launch": F / 1e12,
+                         **at_clock(ach, PEAK_TFLOPS[args.dtype], r["clock"])}}
 
 
 def fp32_secondary(args, dev, bags=64, steps=10, warmup=2):
@@ -406,7 +482,8 @@ def fp32_secondary(args, dev, bags=64, steps=10, warmup=2):
                          "kernel": (f"gate_fused_kernel ({r['regions']} regions)" if r["fused"]
                                     else "gate_pipe_kernel (fp32 MFMA 16x16x4)"),
                          "timed_path": "fused: gate+softmax+pooling" if r["fused"] else "two-kernel: gate only",
-                         "algorithmic_tflop_per_launch": F / 1e12}}
+                         "algorithmic_tflop_per_launch": F / 1e12,
+                         **at_clock(ach, PEAK_TFLOPS["f32"], r["clock"])}}
 
 
 def single_bag_line(args, dev, quiet=False):

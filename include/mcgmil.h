@@ -49,7 +49,7 @@ extern "C" {
 
 #define MCGMIL_ABI_VERSION 4   /* 2: mcgmil_args.flags (path selection); 3: mcgmil_conv_args.flags,
                                   mcgmil_stem_args.flags (mcgmil_features.h); 4: MCGMIL_GATE_ROW and
-                                  the row-gate weight stream in the packed weights */
+                                  the row-gate weight stream in the packed weights, MCGMIL_CLOCK_PROBE */
 
 enum mcgmil_status {
     MCGMIL_OK = 0,
@@ -79,8 +79,14 @@ enum mcgmil_flags {
     MCGMIL_GATE_PP = 2 << 2,     /* gate_pp_kernel (two 4-wave workgroups per CU) where it applies */
     MCGMIL_GATE_ROW = 3 << 2,    /* rowgate_scores_kernel (one wave per SIMD, each wave owns whole
                                     rows; bf16, D % 32 == 0, <= 16 gate column blocks of 32) */
-    MCGMIL_GATE_MASK = 3 << 2
+    MCGMIL_GATE_MASK = 3 << 2,
+    MCGMIL_CLOCK_PROBE = 1 << 4  /* measurement: the gate launch's workgroups 0..MCGMIL_CLOCK_SLOTS-1
+                                    write their (s_memtime, s_memrealtime) at start and end into
+                                    args->debug ([MCGMIL_CLOCK_SLOTS][4] uint64, required): the shader
+                                    clock the launch ran at = d(memtime) / d(realtime) x 100 MHz.
+                                    Outputs are unchanged; no stamp executes without the flag */
 };
+#define MCGMIL_CLOCK_SLOTS 1024
 
 typedef struct mcgmil_args {
     /* ---- sizes ---- */
@@ -128,8 +134,8 @@ typedef struct mcgmil_args {
     /* ---- scratch ---- */
     void* workspace;      /* >= mcgmil_workspace_size() bytes, 256-byte aligned */
     size_t workspace_bytes;
-    void* debug;          /* diagnostic builds only (-DMCGMIL_STAMPS): per-tile s_memtime
-                             stamps; ignored by the product build. NULL otherwise */
+    void* debug;          /* with MCGMIL_CLOCK_PROBE: the clock record; diagnostic builds
+                             (-DMCGMIL_STAMPS): per-tile s_memtime stamps. NULL otherwise */
     /* ---- policy ---- */
     int32_t flags;        /* mcgmil_flags: MCGMIL_PATH_* | MCGMIL_GATE_* (0 = auto) */
     int32_t reserved;     /* must be 0 */

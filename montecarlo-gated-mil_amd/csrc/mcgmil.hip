@@ -102,9 +102,11 @@ int validate_batch(const mcgmil_args* a) {
         return fail(MCGMIL_E_INVALID, "uniform_bag_rows must be 0 or total_rows / num_bags");
     if (!(a->p_feat >= 0.f && a->p_feat <= 1.f) || !(a->p_att >= 0.f && a->p_att <= 1.f))
         return fail(MCGMIL_E_INVALID, "dropout probabilities must be in [0, 1]");
-    if ((a->flags & ~(MCGMIL_PATH_MASK | MCGMIL_GATE_MASK)) != 0 || (a->flags & MCGMIL_PATH_MASK) == 3 ||
-        a->reserved != 0)
-        return fail(MCGMIL_E_INVALID, "flags must be MCGMIL_PATH_* | MCGMIL_GATE_* and reserved 0");
+    if ((a->flags & ~(MCGMIL_PATH_MASK | MCGMIL_GATE_MASK | MCGMIL_CLOCK_PROBE)) != 0 ||
+        (a->flags & MCGMIL_PATH_MASK) == 3 || a->reserved != 0)
+        return fail(MCGMIL_E_INVALID, "flags must be MCGMIL_PATH_* | MCGMIL_GATE_* [| MCGMIL_CLOCK_PROBE] and reserved 0");
+    if ((a->flags & MCGMIL_CLOCK_PROBE) && !a->debug)
+        return fail(MCGMIL_E_INVALID, "MCGMIL_CLOCK_PROBE needs args->debug ([MCGMIL_CLOCK_SLOTS][4] uint64)");
     return MCGMIL_OK;
 }
 
@@ -184,6 +186,8 @@ int launch_gate_generic(const mcgmil::GateParams& gp, hipStream_t s) {
 template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE>
 int launch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
     auto* k = &mcgmil::gate_pipe_kernel<E, PPW, MAXC, REPLAY, ONE>;
+    if constexpr (!REPLAY)
+        if (gp.clock) k = &mcgmil::gate_pipe_kernel<E, PPW, MAXC, REPLAY, ONE, true>;   // MCGMIL_CLOCK_PROBE
     if (int rc = mcgmil_detail::raise_lds_limit(reinterpret_cast<const void*>(k), "gate_pipe_kernel LDS limit"))
         return rc;
     const long long tiles = (gp.total_samples + mcgmil::kPipeBM - 1) / mcgmil::kPipeBM;
@@ -200,6 +204,8 @@ template <typename E, int RT, int PPW, int MAXC, bool REPLAY, bool ONE>
 int launch_gate_pp(const mcgmil::GateParams& gp, hipStream_t s) {
     constexpr int BM = 16 * RT;
     auto* k = &mcgmil::gate_pp_kernel<E, RT, PPW, MAXC, REPLAY, ONE>;
+    if constexpr (!REPLAY)
+        if (gp.clock) k = &mcgmil::gate_pp_kernel<E, RT, PPW, MAXC, REPLAY, ONE, true>;   // MCGMIL_CLOCK_PROBE
     const long long tiles = (gp.total_samples + BM - 1) / BM;
     if (tiles == 0) return MCGMIL_OK;
     if (gp.uniform_rows <= 0)
@@ -511,7 +517,13 @@ int gate_params(const mcgmil_args* a, mcgmil::GateParams& gp) {
     gp.keep_att = a->keep_att;
     gp.logits = reinterpret_cast<float*>(static_cast<char*>(a->workspace) + l.logits_off);
     gp.zz = reinterpret_cast<float*>(static_cast<char*>(a->workspace) + l.zz_off);
+#ifdef MCGMIL_STAMPS
     gp.stamps = static_cast<unsigned long long*>(a->debug);
+    gp.clock = nullptr;
+#else
+    gp.stamps = nullptr;
+    gp.clock = (a->flags & MCGMIL_CLOCK_PROBE) ? static_cast<unsigned long long*>(a->debug) : nullptr;
+#endif
     gp.tile_bag = reinterpret_cast<const int32_t*>(static_cast<char*>(a->workspace) + l.plan_off);
     gp.uniform_rows = a->uniform_bag_rows;
     gp.Y = a->Y;

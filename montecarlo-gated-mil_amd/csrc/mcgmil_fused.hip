@@ -59,7 +59,8 @@ namespace {
 
 template <typename E, int PPW, int MAXC, bool ONE>
 int launch(const mcgmil::GateParams& gp, long long total_rows, hipStream_t s) {
-    auto* k = &mcgmil::gate_fused_kernel<E, PPW, MAXC, ONE>;
+    auto* k = gp.clock ? &mcgmil::gate_fused_kernel<E, PPW, MAXC, ONE, true>   // MCGMIL_CLOCK_PROBE
+                       : &mcgmil::gate_fused_kernel<E, PPW, MAXC, ONE>;
     if (int rc = raise_lds_limit(reinterpret_cast<const void*>(k), "gate_fused_kernel LDS limit")) return rc;
     constexpr int cap = mcgmil::fused_cap<MAXC>();
     if (gp.uniform_rows <= 0) {

@@ -49,7 +49,7 @@ __host__ __device__ constexpr size_t pp_lds_bytes() {
            + (size_t)kRowInfo * 16 * RT * 4;                    // row table
 }
 
-template <typename E, int RT, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS>
+template <typename E, int RT, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS, bool PROBE = false>
 __global__ __launch_bounds__(kPPThreads, 2) void gate_pp_kernel(const GateParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     static_assert(RT % kPPWaves == 0, "row tiles must split over the waves");
@@ -66,6 +66,7 @@ __global__ __launch_bounds__(kPPThreads, 2) void gate_pp_kernel(const GateParams
     int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);
     const long long R0 = (long long)blockIdx.x * BM;
 
+    if constexpr (PROBE) clock_probe(p, 0);
     MCGMIL_STAMP(p, 0);
     fill_row_table<BM>(p, R0, rinfo);
     __syncthreads();
@@ -272,6 +273,7 @@ __global__ __launch_bounds__(kPPThreads, 2) void gate_pp_kernel(const GateParams
         p.zz[o] = zred[c * BM + r] * p.sf;
     }
     MCGMIL_STAMP(p, 7);
+    if constexpr (PROBE) clock_probe(p, 1);
 }
 
 }  // namespace mcgmil

@@ -50,7 +50,23 @@ struct GateParams {
     const int32_t* region_off;     // [B+1] prefix of per-bag region counts (ragged bags) or nullptr
     int region_t;                  // t-groups per region when every bag has uniform_rows rows
     unsigned long long* stamps;    // diagnostic build only: [tiles][8] s_memtime stamps
+    unsigned long long* clock;     // MCGMIL_CLOCK_PROBE: [kClockSlots][4] clock record, or nullptr
 };
+
+// The clock probe (MCGMIL_CLOCK_PROBE): thread 0 of workgroups 0..kClockSlots-1 writes
+// (s_memtime, s_memrealtime) at its start (i = 0) and end (i = 1). Nothing is kept live in
+// between: the marks go to memory at once (vector stores). The tile kernels compile it into a
+// separate PROBE instantiation, launched only for a probed call: even an untaken branch at the
+// kernel's ends re-schedules gate_fused_kernel's tile loop (-11% measured, profiles/r05).
+constexpr int kClockSlots = 1024;
+__device__ __forceinline__ void clock_probe(const GateParams& p, int i) {
+    if (p.clock && threadIdx.x == 0 && blockIdx.x < (unsigned)kClockSlots) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+        p.clock[(size_t)blockIdx.x * 4 + 2 * i] = t;
+        p.clock[(size_t)blockIdx.x * 4 + 2 * i + 1] = r;
+    }
+}
 
 // In-kernel phase stamps (diagnostic build, -DMCGMIL_STAMPS; compiled out otherwise): lane 0
 // of wave 0 records s_memtime into stamps[tile * 8 + i].
@@ -802,7 +818,7 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
     MCGMIL_STAMP(p, 7);
 }
 
-template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS>
+template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS, bool PROBE = false>
 __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int BM = kPipeBM;
@@ -812,11 +828,13 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);
     const long long R0 = (long long)blockIdx.x * BM;
 
+    if constexpr (PROBE) clock_probe(p, 0);
     MCGMIL_STAMP(p, 0);
     fill_row_table<BM>(p, R0, rinfo);
     __syncthreads();
     MCGMIL_STAMP(p, 1);
     pipe_tile<E, PPW, MAXC, REPLAY, ONE_CLASS>(p, R0, Xs, red, zred, rinfo, p.logits, p.zz, 0);
+    if constexpr (PROBE) clock_probe(p, 1);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -961,7 +979,7 @@ __device__ __forceinline__ void fill_row_table_region(const GateParams& p, const
 }
 
 
-template <typename E, int PPW, int MAXC, bool ONE_CLASS>
+template <typename E, int PPW, int MAXC, bool ONE_CLASS, bool PROBE = false>
 __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GateParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int BM = kPipeBM;
@@ -985,6 +1003,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GatePara
 #endif
     Region rg;
     if (!decode_region(p, (int)blockIdx.x, CAP, rg)) return;   // grid rounded up (ragged bags)
+    if constexpr (PROBE) clock_probe(p, 0);
     const int ntiles = (int)((rg.rows + BM - 1) / BM);
     // The tile loop keeps almost nothing in registers across tiles: the region sits in LDS and
     // the parameters are re-read from the kernarg segment in every tile, both through pointers
@@ -1037,6 +1056,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_fused_kernel(const GatePara
         float* Yo = p.Y + ((size_t)rg.bag * p.T + rg.t0 + j) * p.C;
         softmax_group(ltid, act, rg.Nb, p.C, lgj, zzj, Ao, Yo, sred + half * 16);
     }
+    if constexpr (PROBE) clock_probe(p, 1);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -618,6 +618,7 @@ __global__ __launch_bounds__(kRgThreads, 1) void rowgate_scores_kernel(const Gat
     constexpr int NCB = 2 * G * DB;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    clock_probe(p, 0);
     __amdgpu_buffer_rsrc_t wrs;
     RgPipe<NCB, MAXC, DMA> pp;
     rg_setup<NCB, MAXC, DMA>(p, smem, wrs, pp);
@@ -642,6 +643,7 @@ __global__ __launch_bounds__(kRgThreads, 1) void rowgate_scores_kernel(const Gat
         RG_STAMP(p, tile, 3);
         rl = rn;
     }
+    clock_probe(p, 1);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -693,6 +695,7 @@ __global__ __launch_bounds__(kRgThreads, 1) void rowgate_fused_kernel(const Gate
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Region rg;
     if (!decode_region(p, (int)blockIdx.x, CAP, rg)) return;   // grid rounded up (ragged bags)
+    clock_probe(p, 0);
     __amdgpu_buffer_rsrc_t wrs;
     RgPipe<NCB, MAXC, DMA> pp;
     rg_setup<NCB, MAXC, DMA>(p, smem, wrs, pp);
@@ -729,6 +732,7 @@ __global__ __launch_bounds__(kRgThreads, 1) void rowgate_fused_kernel(const Gate
         float* Yo = p.Y + ((size_t)rg.bag * p.T + rg.t0 + j) * p.C;
         softmax_group(threadIdx.x, true, rg.Nb, p.C, lgj, zzj, Ao, Yo, sred);
     }
+    clock_probe(p, 1);
 }
 
 }  // namespace mcgmil

@@ -15,7 +15,7 @@ SOURCES = ["mcgmil.hip", "mcgmil_fused.hip", "mcgmil_image.hip", "mcgmil_bn.hip"
            "mcgmil_conv32.hip"]
 DEPS = ["mcgmil.hip", "mcgmil_fused.hip", "mcgmil_fused.h", "mcgmil_image.hip", "mcgmil_bn.hip", "mcgmil_conv.hip", "mcgmil_stem.hip",
         "mcgmil_conv32.hip", "mcgmil_kernels.h",
-        "mcgmil_device.h", "mcgmil_error.h", "mcgmil_gate_pp.h"]
+        "mcgmil_device.h", "mcgmil_error.h", "mcgmil_gate_pp.h", "mcgmil_rowgate.h"]
 ARCH = os.environ.get("MCGMIL_OFFLOAD_ARCH", "gfx950")
 # No packed-fp32 VALU (v_pk_fma/mul/add_f32): with ROCm 7.2's compiler a packed write into the
 # source VGPR of a just-issued v_rcp_f32 / v_exp_f32 gets no wait states, and on gfx950 the

@@ -25,6 +25,8 @@ PATH_FLAGS = {"auto": 0, "fused": 1, "two_kernel": 2}
 CONV_TILE_FLAGS = {"auto": 0, "nohalo": 1, "small": 2, "big512": 3}
 STEM_POOL_UNSPLIT = 1
 GATE_FLAGS = {"auto": 0, "pipe": 1 << 2, "pp": 2 << 2, "row": 3 << 2}
+CLOCK_PROBE = 1 << 4         # MCGMIL_CLOCK_PROBE: clock record of the gate launch into args.debug
+CLOCK_SLOTS = 1024           # MCGMIL_CLOCK_SLOTS: [slots][4] uint64
 
 EXPORTED = (
     "mcgmil_abi_version", "mcgmil_args_size", "mcgmil_last_error", "mcgmil_workspace_size",
@@ -153,9 +155,10 @@ def load():
     return _lib
 
 
-def bind(path: str, mcdo_only: bool = False):
+def bind(path: str, mcdo_only: bool = False, any_abi: bool = False):
     """dlopen a build of the library and declare its entry points. mcdo_only: a gate-kernel A/B
-    build (scripts/build_variants.sh with GATE_ONLY=1) that holds the MCDO entry points only."""
+    build (scripts/build_variants.sh with GATE_ONLY=1) that holds the MCDO entry points only;
+    any_abi: an A/B build of an earlier revision (same mcgmil_args layout, older ABI number)."""
     L = ctypes.CDLL(path)
     pa = ctypes.POINTER(Args)
     L.mcgmil_abi_version.restype = ctypes.c_int
@@ -178,7 +181,7 @@ def bind(path: str, mcdo_only: bool = False):
         f = getattr(L, name)
         f.argtypes = [pa, _vp, _vp]
         f.restype = ctypes.c_int
-    if L.mcgmil_abi_version() != ABI_VERSION:
+    if L.mcgmil_abi_version() != ABI_VERSION and not any_abi:
         raise MCGMILError(f"ABI mismatch: {path} has ABI version {L.mcgmil_abi_version()}, "
                           f"the binding expects {ABI_VERSION}")
     if L.mcgmil_args_size() != ctypes.sizeof(Args):

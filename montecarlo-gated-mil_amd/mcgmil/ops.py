@@ -234,6 +234,26 @@ def mcdo_forward(H: torch.Tensor, bag_offsets: torch.Tensor, head: HeadTensors, 
     return out
 
 
+def clock_record(device) -> torch.Tensor:
+    """A zeroed MCGMIL_CLOCK_PROBE record (args.debug): int64 [MCGMIL_CLOCK_SLOTS, 4]."""
+    return torch.zeros(_lib.CLOCK_SLOTS, 4, dtype=torch.int64, device=device)
+
+
+def clock_mhz(record: torch.Tensor) -> Optional[dict]:
+    """The shader clock a probed gate launch ran at: per workgroup d(s_memtime) / d(s_memrealtime)
+    x 100 MHz (the realtime counter's rate) over the workgroups that wrote a record; the median
+    and the spread. None when no workgroup wrote one."""
+    r = record.cpu().double()
+    dt, dr = r[:, 2] - r[:, 0], r[:, 3] - r[:, 1]
+    ok = (dr > 0) & (dt > 0)
+    if not bool(ok.any()):
+        return None
+    mhz = (dt[ok] / dr[ok] * 100.0).sort().values
+    n = mhz.numel()
+    return {"median": float(mhz[n // 2]), "p10": float(mhz[n // 10]), "p90": float(mhz[(9 * n) // 10]),
+            "workgroups": n, "median_span_us": float((dr[ok] / 100.0).median())}
+
+
 def split_bags(flat: torch.Tensor, sizes: Sequence[int], per_row: int):
     """Split a per-row flat output (A: per_row = T*C; A_mean: per_row = C) into bag views."""
     out, o = [], 0

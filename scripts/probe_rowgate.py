@@ -92,7 +92,7 @@ def timing(dev):
     # with gate="row" beside the product library's default kernel
     paths = [q for q in os.environ.get("MCGMIL_PROBE_LIBS", "").split(",") if q]
     libs = {"product": lib}
-    libs.update({os.path.basename(q): _lib.bind(q, mcdo_only=True) for q in paths})
+    libs.update({os.path.basename(q): _lib.bind(q, mcdo_only=True, any_abi=True) for q in paths})
     N, T, L, D, C = 2048, 100, 512, 128, 2
     B = int(os.environ.get("PROBE_BAGS", "64"))
     rounds, iters = 7, 3
@@ -106,9 +106,13 @@ def timing(dev):
         G = 1 if shared else C
         head = head_on(synthetic.head_arrays(synthetic.head_state_dict(0, C=C, shared=shared), C, shared), dev)
         packed = ops.packed_weights(head, torch.bfloat16)
-        combos = [(n, "row", "two_kernel") for n in libs] + [("product", "auto", "two_kernel")]
-        if not shared:
-            combos += [("product", "row", "fused"), ("product", "auto", "fused")]
+        # PROBE_VARIANT="gate:path" times the variant libraries on that launch (default row two-kernel)
+        vg, vp = os.environ.get("PROBE_VARIANT", "row:two_kernel").split(":")
+        combos = [(n, vg if n != "product" else "row", vp if n != "product" else "two_kernel") for n in libs]
+        combos += [("product", "auto", "two_kernel")]
+        combos += [("product", "row", "fused"), ("product", "auto", "fused")]
+        if shared:   # the tile kernels: gate_pipe_kernel / gate_fused_kernel (one pair per wave)
+            combos += [("product", "pipe", "two_kernel"), ("product", "pipe", "fused")]
         for name, gate, path in combos:
             if paths and shared and os.environ.get("PROBE_SHARED", "1") == "0":
                 continue

@@ -87,7 +87,7 @@ def test_workspace_size_formula(hip_lib):
     ("L", 500, -2), ("L", 4096, -2), ("D", 100, -2), ("C", 5, -2), ("C", 0, -2), ("G", 3, -1),
     ("T", 0, -1), ("num_bags", 0, -1), ("p_feat", 1.5, -1), ("p_att", -0.1, -1),
     ("h_dtype", 7, -1), ("bag_offsets", None, -1), ("total_rows", -1, -1),
-    ("flags", 3, -1), ("flags", 16, -1), ("reserved", 1, -1),
+    ("flags", 3, -1), ("flags", 16, -1), ("flags", 32, -1), ("reserved", 1, -1),
 ])
 def test_validation_errors(hip_lib, field, value, code):
     rc, _ = _ws(hip_lib, _args(**{field: value}))
