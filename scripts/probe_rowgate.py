@@ -95,7 +95,7 @@ def timing(dev):
     libs.update({os.path.basename(q): _lib.bind(q, mcdo_only=True, any_abi=True) for q in paths})
     N, T, L, D, C = 2048, 100, 512, 128, 2
     B = int(os.environ.get("PROBE_BAGS", "64"))
-    rounds, iters = 7, 3
+    rounds, iters = 7, int(os.environ.get("PROBE_ITERS", "3"))
     g = torch.Generator(device=dev).manual_seed(0)
     H = torch.randn(B * N, L, device=dev, generator=g).abs_().bfloat16().contiguous()
     offs = ops.bag_offsets_tensor([N] * B, dev)
