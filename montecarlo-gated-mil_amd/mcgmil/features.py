@@ -251,7 +251,6 @@ def conv2d_f32(conv: nn.Conv2d, x: torch.Tensor, stats: bool = False,
                          "convolution with out_channels % 64 == 0 (conv32_fusable)")
     L = _lib.load()
     a = _conv_args(conv, x)
-    a.flags = int(flags)
     if in_ab is not None:
         if in_ab.shape != (2, a.in_channels) or in_ab.dtype != torch.float32 or \
                 in_ab.device != x.device or not in_ab.is_contiguous():
