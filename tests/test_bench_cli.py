@@ -42,3 +42,15 @@ def test_gpus_flag_spawns_ranks(cuda):
     assert out["n_gpus"] == 2
     assert out["config"]["global_batch_bags"] == 8
     assert out["value"] > 0
+
+
+def test_cpu_baseline_core_count_has_provenance():
+    """cpu_baseline times the reference on every CPU this process may use: its affinity mask,
+    capped by the cgroup CPU quota; the line records both (verdict r04, item 7)."""
+    sys.path.insert(0, REPO)
+    import bench
+    n, prov = bench.host_cores()
+    assert prov["affinity_cpus"] == len(os.sched_getaffinity(0))
+    assert 1 <= n <= prov["affinity_cpus"]
+    if prov["cgroup_cpu_quota"] is not None:
+        assert n <= max(1, int(prov["cgroup_cpu_quota"]))

@@ -383,3 +383,49 @@ def test_random_shapes_fused_two_kernel_oracle(cuda, case):
         np.testing.assert_allclose(Y[b], Yr[:, 0].numpy(), rtol=0, atol=tol["Y"])
         Ar = Ar[:, 0].numpy()
         assert np.abs(A[b].numpy().reshape(T, C, n) - Ar).max() <= tol["A"] * max(np.abs(Ar).max(), 1e-30)
+
+
+@pytest.mark.parametrize("path,shared", [("fused", False), ("two_kernel", False), ("two_kernel", True)])
+def test_clock_probe(cuda, path, shared):
+    """MCGMIL_CLOCK_PROBE (the clock bench.py states in every roofline): the probed launch runs the
+    PROBE instantiation of the same tile kernel -- outputs bitwise equal to the unprobed launch --
+    and every workgroup that owns a record slot writes start/end (s_memtime, s_memrealtime) stamps
+    from which a plausible shader clock follows."""
+    import ctypes
+    from mcgmil import _lib, ops
+    B, N, T = (128, 256, 100) if path == "fused" else (4, 700, 20)
+    sd = synthetic.head_state_dict(8, C=2, shared=shared)
+    head = head_on(synthetic.head_arrays(sd, 2, shared), cuda)
+    H = torch.rand(B * N, 512, device=cuda).bfloat16()
+    offs = ops.bag_offsets_tensor([N] * B, cuda)
+    packed = ops.packed_weights(head, torch.bfloat16)      # the stages need packed weights
+    outs = []
+    for probe in (False, True):
+        a = ops.make_args(H, offs, head, T, 2, head.G, 128, 0.1, 0.1, seed=3, path=path)
+        a.packed_w = ctypes.c_void_p(packed.data_ptr())
+        n = ctypes.c_size_t()
+        lib = _lib.load()
+        _lib.check(lib.mcgmil_workspace_size(ctypes.byref(a), ctypes.byref(n)), "ws")
+        ws = torch.empty(n.value, dtype=torch.uint8, device=cuda)
+        a.workspace, a.workspace_bytes = ctypes.c_void_p(ws.data_ptr()), n.value
+        Y = torch.empty(B, T, 2, device=cuda)
+        A = torch.empty(T * 2 * B * N, device=cuda)
+        a.Y, a.A = ctypes.c_void_p(Y.data_ptr()), ctypes.c_void_p(A.data_ptr())
+        rec = ops.clock_record(cuda)
+        if probe:
+            a.debug, a.flags = ctypes.c_void_p(rec.data_ptr()), a.flags | _lib.CLOCK_PROBE
+        regions = ctypes.c_int64()
+        _lib.check(lib.mcgmil_fused_regions(ctypes.byref(a), ctypes.byref(regions)), "regions")
+        assert (regions.value > 0) == (path == "fused")
+        sh = ctypes.c_void_p(torch.cuda.current_stream(cuda).cuda_stream)
+        _lib.check(lib.mcgmil_gate_softmax_pool(ctypes.byref(a), sh), "gate_softmax_pool")
+        torch.cuda.synchronize()
+        outs.append((Y.clone(), A.clone(), rec.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert int(torch.count_nonzero(outs[0][2])) == 0          # no probe: nothing written
+    r = outs[1][2]
+    wrote = int(((r[:, 2] > r[:, 0]) & (r[:, 3] > r[:, 1])).sum())
+    grid = regions.value if path == "fused" else (T * B * N + 127) // 128
+    assert wrote == min(grid, _lib.CLOCK_SLOTS)
+    c = ops.clock_mhz(outs[1][2])
+    assert c is not None and 500.0 < c["median"] < 3000.0, c
