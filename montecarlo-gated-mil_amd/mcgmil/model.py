@@ -88,16 +88,30 @@ class MultiHeadGatedAttentionMIL(nn.Module):
             return [self.attention_V[0]], [self.attention_U[0]]
         return [m[0] for m in self.attention_V], [m[0] for m in self.attention_U]
 
-    def head_tensors(self, device) -> ops.HeadTensors:
-        """The head parameters stacked for the kernel (cached until a parameter changes)."""
+    def _head_params(self):
+        """The head's parameters in kernel order, cached per module structure (the per-bag caller of
+        infer.py:187-191 would otherwise walk nn.Module attribute lookups on every call)."""
+        mods = self._modules
+        skey = (self.shared_attention, id(mods.get("attention_V")), id(mods.get("attention_U")),
+                id(mods.get("attention_weights")), id(mods.get("classifiers")))
+        hit = self.__dict__.get("_head_param_cache")
+        if hit is not None and hit[0] == skey:
+            return hit[1]
         lv, lu = self._gate_linears()
         params = [p for m in lv + lu for p in (m.weight, m.bias)]
         params += [p for m in self.attention_weights for p in (m.weight, m.bias)]
         params += [m.weight for m in self.classifiers]
+        self.__dict__["_head_param_cache"] = (skey, params)
+        return params
+
+    def head_tensors(self, device) -> ops.HeadTensors:
+        """The head parameters stacked for the kernel (cached until a parameter changes)."""
+        params = self._head_params()
         key = (str(device), self.compute_dtype,
                tuple((p.data_ptr(), p._version) for p in params))
         if self._head_cache is not None and self._head_cache[0] == key:
             return self._head_cache[1], self._head_cache[2]
+        lv, lu = self._gate_linears()
         with torch.no_grad():
             f32 = dict(device=device, dtype=torch.float32)
             head = ops.HeadTensors(

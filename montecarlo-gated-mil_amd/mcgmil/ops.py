@@ -61,19 +61,31 @@ def _require_cuda(name, t, dtype=None):
         raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
 
 
+_CHECKED_HEADS: dict = {}     # id -> (head, device): heads already validated (per-call host time)
+
+
 def _check_head(head: HeadTensors, device):
+    hit = _CHECKED_HEADS.get(id(head))
+    if hit is not None and hit[0] is head and hit[1] == device:
+        return                    # same tensors: dtype, layout and device cannot have changed
     for name, t in zip(head._fields, head):
         _require_cuda(name, t, torch.float32)
         if not t.is_contiguous():
             raise ValueError(f"{name} must be contiguous")
         if t.device != device:
             raise ValueError(f"{name} is on {t.device}, H on {device}")
+    if len(_CHECKED_HEADS) > 16:
+        _CHECKED_HEADS.clear()
+    _CHECKED_HEADS[id(head)] = (head, device)
 
 
 class BagOffsets(torch.Tensor):
     """int32 CSR offsets [B+1] on the device that remember, from the host-side sizes they were
-    built from, whether every bag has the same size (`uniform_rows`, 0 if ragged)."""
+    built from, whether every bag has the same size (`uniform_rows`, 0 if ragged). No torch-function
+    override: methods dispatch as on a plain tensor (and return plain tensors), so the subclass
+    costs the per-call path nothing."""
     uniform_rows: int = 0
+    __torch_function__ = torch._C._disabled_torch_function_impl
 
 
 def uniform_offsets(n: int, bags: int, device) -> torch.Tensor:
