@@ -375,34 +375,41 @@ int try_fused_maxc(const mcgmil::GateParams& gp, long long total_rows, int L, in
     *rc = MCGMIL_OK;
     // (L >= 128: the fused pipeline peels two K steps at each end of a tile)
     if (gp.keep_feat) return 0;
-    bool row = false;
+    bool row = false, pp = false;
     if constexpr (sizeof(E) == 2) {       // bf16: the kernel dispatch_gate_maxc would pick
         const int mode = gate_mode(flags);
         row = mode == 3 && rowgate_applies(gp) &&
               mcgmil::rg_fused_lds_bytes<2 * 2 * 4, MAXC>(L, gp.G, gp.C, gp.D) <= 160 * 1024;
         const bool pipe = mode == 1 || (mode == 0 && gp.P > 2 * mcgmil::kPPWaves);
-        if (!row && !pipe) return 0;
+        // gate_pp_kernel's heads (<= 8 gate tile pairs: shared heads) fuse on its own tile
+        pp = !row && !pipe && gp.P <= 2 * mcgmil::kPPWaves && L % 64 == 0 && L >= 128;
+        if (!row && !pipe && !pp) return 0;
     }
-    if (!row && (L % 64 != 0 || L < 128 || gp.P > 2 * mcgmil::kGateWaves)) return 0;
-    if (!row && mcgmil::fused_kernel_lds_bytes<E, MAXC>(L) > 160 * 1024) return 0;   // bf16 L > 1024
+    if (!row && !pp && (L % 64 != 0 || L < 128 || gp.P > 2 * mcgmil::kGateWaves)) return 0;
+    if (!row && !pp && mcgmil::fused_kernel_lds_bytes<E, MAXC>(L) > 160 * 1024) return 0;   // bf16 L > 1024
     const int fm = fused_mode(flags);
     if (fm == 0) return 0;
+    const int cap = pp ? mcgmil::pp_fused_cap<MAXC>() : mcgmil::fused_cap<MAXC>();
     // auto: bf16 uniform batches only -- on ragged ones (config 4) the fused launch measured 2.8%
     // slower (regions of 16-32 tiles straddling t-groups; profiles/r03/bench_cfg4*.log), and in fp32
     // (which spills in the tile loop) 13-18% slower (profiles/r03/probe_fused_f32.log)
-    if (fm < 0 && (sizeof(E) != 2 || gp.uniform_rows <= 0 ||
-                   mcgmil_detail::fused_regions(gp, total_rows, mcgmil::fused_cap<MAXC>(), true) <
-                       kFusedMinRegions))
+    // gate_pp_fused_kernel: opt-in only -- 16.68 vs 16.56 ms for the two-kernel path on 256 shared-head
+    // bags of config 3 (profiles/r05/pp_fused_probe.log)
+    if (fm < 0 && (pp || sizeof(E) != 2 || gp.uniform_rows <= 0 ||
+                   mcgmil_detail::fused_regions(gp, total_rows, cap, true) < kFusedMinRegions))
         return 0;
     // same kernel shape as dispatch_gate_pipe: one class per wave for separate heads
-    const int ppw = gp.P <= mcgmil::kGateWaves ? 1 : 2;
+    const int ppw = pp ? 2 : gp.P <= mcgmil::kGateWaves ? 1 : 2;   // (gate_pp: dispatch_gate_pp<8, 2>)
     const bool one = gp.G > 1 && gp.G == gp.C && (gp.D / 16) % ppw == 0;
     if (regions) {
-        *regions = mcgmil_detail::fused_regions(gp, total_rows, mcgmil::fused_cap<MAXC>(), false);
+        mcgmil::GateParams g2 = gp;
+        if (pp) g2.region_t = gp.uniform_rows > 0 ? mcgmil::region_t_groups(gp.uniform_rows, gp.T, cap) : 0;
+        *regions = mcgmil_detail::fused_regions(g2, total_rows, cap, false);
         return 1;
     }
-    *rc = row ? mcgmil_detail::launch_rowgate_fused(gp, MAXC, total_rows, s)
-              : mcgmil_detail::launch_gate_fused(gp, sizeof(E) == 2, ppw, MAXC, one, total_rows, s);
+    *rc = row  ? mcgmil_detail::launch_rowgate_fused(gp, MAXC, total_rows, s)
+          : pp ? mcgmil_detail::launch_pp_fused(gp, MAXC, one, total_rows, s)
+               : mcgmil_detail::launch_gate_fused(gp, sizeof(E) == 2, ppw, MAXC, one, total_rows, s);
     return 1;
 }
 

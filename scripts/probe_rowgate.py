@@ -4,6 +4,8 @@ timing against the current kernels interleaved in one process.
 
   PROBE_PARITY=0   skip the parity part
   PROBE_BAGS       bags per timed launch (default 64 of N = 2048, T = 100)
+  PROBE_VARIANT    "gate:path" the variant libraries (MCGMIL_PROBE_LIBS) are timed on; path "pool2" is
+                   the two-kernel path through mcgmil_gate_softmax_pool
 Prints one JSON line per check / variant.
 """
 import ctypes
@@ -110,13 +112,15 @@ def timing(dev):
         vg, vp = os.environ.get("PROBE_VARIANT", "row:two_kernel").split(":")
         combos = [(n, vg if n != "product" else "row", vp if n != "product" else "two_kernel") for n in libs]
         combos += [("product", "auto", "two_kernel")]
-        combos += [("product", "row", "fused"), ("product", "auto", "fused")]
+        combos += [("product", "row", "fused"), ("product", "auto", "fused"), ("product", "auto", "pool2")]
         if shared:   # the tile kernels: gate_pipe_kernel / gate_fused_kernel (one pair per wave)
             combos += [("product", "pipe", "two_kernel"), ("product", "pipe", "fused")]
         for name, gate, path in combos:
             if paths and shared and os.environ.get("PROBE_SHARED", "1") == "0":
                 continue
-            a = ops.make_args(H, offs, head, T, C, G, D, 0.1, 0.1, seed=1, gate=gate, path=path)
+            # path "pool2": the two-kernel path through mcgmil_gate_softmax_pool (gate + softmax launches)
+            a = ops.make_args(H, offs, head, T, C, G, D, 0.1, 0.1, seed=1, gate=gate,
+                              path="two_kernel" if path == "pool2" else path)
             a.packed_w = ctypes.c_void_p(packed.data_ptr())
             n = ctypes.c_size_t()
             _lib.check(lib.mcgmil_workspace_size(ctypes.byref(a), ctypes.byref(n)), "ws")
@@ -131,7 +135,7 @@ def timing(dev):
     for _ in range(rounds):
         for k, (a, *_rest) in setups.items():
             lb = setups[k][5]
-            fn = lb.mcgmil_gate_softmax_pool if k[3] == "fused" else lb.mcgmil_gate_scores
+            fn = lb.mcgmil_gate_softmax_pool if k[3] in ("fused", "pool2") else lb.mcgmil_gate_scores
             _lib.check(fn(ctypes.byref(a), sh), "gate")
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -143,7 +147,7 @@ def timing(dev):
     for (shared, gate, name, path), ts in times.items():
         ms = statistics.median(ts)
         flops = setups[(shared, gate, name, path)][4]
-        print(json.dumps({"timing": "gate_softmax_pool" if path == "fused" else "gate_scores", "lib": name,
+        print(json.dumps({"timing": "gate_softmax_pool" if path in ("fused", "pool2") else "gate_scores", "lib": name,
                           "shared": shared, "gate": gate, "path": path, "bags": B,
                           "ms": round(ms, 4),
                           "tflops": round(flops / (ms * 1e-3) / 1e12, 1),

@@ -101,6 +101,18 @@ def test_fused_kernel_fits_without_spills(fused_asm):
         assert kernel_meta(fused_asm, sym, "num_vgpr") + kernel_meta(fused_asm, sym, "num_agpr") <= 256, sym
 
 
+def test_pp_fused_kernel_fits(fused_asm):
+    # gate_pp_fused_kernel (opt-in single launch for shared heads): two workgroups per CU, so <= 256
+    # registers; the Philox instantiations keep one 8-byte value in scratch, stored before the tile
+    # loop and reloaded once per 128-row tile outside the K loop (12 bytes of frame) -- more would mean
+    # spills in the tile code itself
+    syms = set(re.findall(r"\.set (_ZN6mcgmil20gate_pp_fused_kernel\w*)\.private_seg_size", fused_asm))
+    assert len(syms) == 4, syms       # MAXC in {2, 4} x one class per wave or not
+    for sym in syms:
+        assert kernel_meta(fused_asm, sym, "private_seg_size") <= 16, sym
+        assert kernel_meta(fused_asm, sym, "num_vgpr") + kernel_meta(fused_asm, sym, "num_agpr") <= 256, sym
+
+
 def _rowgate_syms(text, kind):
     return set(re.findall(rf"\.set (_ZN6mcgmil\d+rowgate_{kind}_kernel\w*)\.private_seg_size", text))
 

@@ -1,6 +1,7 @@
-"""The single-launch hot path (gate_fused_kernel via mcgmil_gate_softmax_pool, reference
-model.py:280-316) against the two-kernel path (gate_pipe_kernel -> workspace ->
-softmax_pool_kernel) and against the reference's golden outputs.
+"""The single-launch hot path (gate_fused_kernel, or gate_pp_fused_kernel for bf16 heads of <= 8
+gate tile pairs, via mcgmil_gate_softmax_pool, reference model.py:280-316) against the two-kernel
+path (gate_pipe_kernel / gate_pp_kernel -> workspace -> softmax_pool_kernel) and against the
+reference's golden outputs.
 
 Both paths run the same tile code and the same softmax_group, so every output must be BITWISE
 equal. The cases cover the fused kernel's region shapes: several t-groups per region (small N),
@@ -50,6 +51,13 @@ CASES = [
     ("f32_shared_uniform_N96", torch.float32, [96] * 5, 40, 2, True, 128),
     ("f32_c4_sep_ragged", torch.float32, [50, 1500, 1024, 1025, 3], 4, 4, False, 64),
     ("bf16_c1_ragged", torch.bfloat16, [33, 4000, 5], 9, 1, False, 128),
+    # bf16 heads of <= 8 gate tile pairs: gate_pp_fused_kernel (regions of <= 2048 rows, C <= 2;
+    # 512 for C = 4), incl. bags over the cap and the one-class-per-wave tile (D = 64 separate heads)
+    ("bf16_shared_uniform_N2048", torch.bfloat16, [2048] * 3, 7, 2, True, 128),
+    ("bf16_shared_uniform_N300", torch.bfloat16, [300] * 4, 30, 2, True, 128),
+    ("bf16_shared_ragged", torch.bfloat16, [300, 0, 5000, 1, 129, 2048, 2049, 777], 5, 2, True, 128),
+    ("bf16_c4_shared_ragged", torch.bfloat16, [50, 1500, 512, 513, 3], 4, 4, True, 128),
+    ("bf16_sep_d64_ragged", torch.bfloat16, [700, 96, 2049, 0], 6, 2, False, 64),
 ]
 
 
@@ -70,10 +78,7 @@ def test_fused_equals_two_kernel_path(cuda, case):
     nreg = regions(H, offs, head, T, path="fused")
     out = ops.mcdo_forward(H, offs, head, T, path="fused", **kw)
     torch.cuda.synchronize()
-    if dtype == torch.bfloat16 and (shared or C == 1):
-        assert nreg == 0           # bf16 heads of <= 8 gate tile pairs run gate_pp_kernel: not fused
-    else:
-        assert nreg > 0
+    assert nreg > 0
     for k in ref:
         assert torch.equal(out[k], ref[k]) or (k == "A_var" and T == 1), k
     # empty bags: Y = 0 (the reference would not produce a bag of 0 instances; the kernel's rule)
@@ -85,7 +90,8 @@ def test_fused_equals_two_kernel_path(cuda, case):
 def test_fused_auto_policy(cuda):
     """path="auto" (the default) takes the fused launch only for bf16 batches of equal-size bags
     with >= 16,384 regions: 16 bags of N=2048, T=100 (800 regions of two t-groups) do not, 512 bags
-    (25,600, the bench's step) do, ragged or fp32 batches do not. path="two_kernel": never."""
+    (25,600, the bench's step) do, ragged, fp32 or bf16 shared-head batches do not.
+    path="two_kernel": never."""
     from mcgmil import ops
     sd = synthetic.head_state_dict(0, C=2, shared=False)
     head = head_on(synthetic.head_arrays(sd, 2, False), cuda)
@@ -105,6 +111,12 @@ def test_fused_auto_policy(cuda):
     offs32 = ops.bag_offsets_tensor([512] * 1280, cuda)
     assert regions(big32, offs32, head, 100) == 0
     assert regions(big32, offs32, head, 100, path="fused") == 1280 * 13
+    # bf16 shared heads (gate_pp_fused_kernel) stay on the two-kernel path under auto (0.7% slower
+    # fused, profiles/r05/pp_fused_probe.log); forced: one t-group of 2048 rows per region
+    sd = synthetic.head_state_dict(0, C=2, shared=True)
+    shead = head_on(synthetic.head_arrays(sd, 2, True), cuda)
+    assert regions(big, big_offs, shead, 100) == 0
+    assert regions(big, big_offs, shead, 100, path="fused") == 512 * 100
 
 
 from test_gpu_parity import BF16_CASES, FP32_CASES, TOL32, TOL_BF16_IN, compare, run  # noqa: E402
@@ -113,8 +125,7 @@ from test_gpu_parity import BF16_CASES, FP32_CASES, TOL32, TOL_BF16_IN, compare,
 @pytest.mark.parametrize("name", FP32_CASES + BF16_CASES)
 def test_fused_matches_reference_goldens(cuda, name):
     """The fused launch (forced) on every reference-made golden MC case, with the kernel's own
-    Philox masks, at the bounds of tests/test_gpu_parity.py (bf16 shared heads are not fused and
-    run the two-kernel path here)."""
+    Philox masks, at the bounds of tests/test_gpu_parity.py (bf16 shared heads: gate_pp_fused_kernel)."""
     case = Case(name)
     bf16 = name in BF16_CASES
     out = run(case, cuda, torch.bfloat16 if bf16 else torch.float32, path="fused")
