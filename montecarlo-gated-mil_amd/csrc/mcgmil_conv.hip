@@ -661,6 +661,216 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
                                           (int)blockIdx.x, 64, 0);
 }
 
+// ---- conv3x3c64_ring_kernel: the same layer-1 convolution on a ring of input rows.
+// conv3x3c64_kernel is vector-issue bound (5 VALU per MFMA): each tile re-DMAs its whole patch
+// (~1.7 loads per input row) with ~20 VALU of address stepping per 1-KiB piece, and each tap
+// read re-derives its XOR-swizzled address. Here:
+//  - LDS holds a ring of 16 padded input rows (R = n (H + 2) + ih + 1; rows 0 and H + 1 of an
+//    image are zeros) at ring row R % 16, CHUNK-MAJOR: chunk c (8 channels) of padded column q at
+//    (R % 16) * 8 KiB + c * 1 KiB + q * 16 (W + 2 <= 64 columns). A tile DMAs only the rows the
+//    previous tile did not need: each input row is loaded once per workgroup.
+//  - One piece = one (row, chunk): wave w loads chunk w of every row, lane = padded column, so a
+//    piece costs one VALU add (row base scalar, column offset per lane fixed) and, with XF, the
+//    wave's a / b coefficients are 16 scalars for the whole kernel.
+//  - A fragment's 16 pixels read one chunk at consecutive columns: 16 consecutive 16-B slots, no
+//    swizzle needed. Columns 0-3 / 12-15 of a fragment take its pixels 0-7 and columns 4-11 pixels
+//    8-15 (ring_px), so every ds_read_b128 lane group (chunk kq for one half, kq + 1 for the other;
+//    the chunk planes are 1 KiB apart) covers 16 distinct slots mod 256 B.
+//  - Tap (kh, kw) and K half ks of a fragment are its per-tile row base for kh plus the immediate
+//    kw * 16 + ks * 4 KiB: no address VALU in the tap loop.
+// The ring holds the rows of two consecutive tiles (the host checks the span <= 16): tile t + 1's
+// new rows load into ring rows tile t does not read, right after the barrier that opens tile t.
+#ifndef MCGMIL_C64_RING
+#define MCGMIL_C64_RING 1          // 0: conv3x3c64_kernel for layer 1 (A/B builds)
+#endif
+constexpr int kRingRows = 16;
+constexpr int kRingCols = 64;
+constexpr int kRingRowBytes = 8 * kRingCols * 16;
+constexpr size_t kRingBytes = (size_t)kRingRows * kRingRowBytes;   // 128 KiB
+__device__ __forceinline__ int ring_px(int c) { return c < 4 ? c : c < 12 ? c + 4 : c - 8; }
+
+template <bool STATS, bool XF>
+__global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const HaloGeom hg) {
+    const ConvGeom& g = hg.g;
+    constexpr int FI = 2, FJ = 4, KSTEPS = 18;          // wave: 64 pixels x 32 channels
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int t0 = (int)((long long)blockIdx.x * hg.tiles / gridDim.x);
+    const int t1 = (int)((long long)(blockIdx.x + 1) * hg.tiles / gridDim.x);
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(g.x, g.x_bytes);
+    const int HP = g.H + 2, OHW = g.OH * g.OW;
+
+    bf16x8 wf[KSTEPS][FI];
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s)
+#pragma unroll
+        for (int i = 0; i < FI; ++i) {
+            const int co = wn * 32 + i * 16 + (lane & 15);
+            wf[s][i] = *reinterpret_cast<const bf16x8*>(g.w + (size_t)co * 576 + s * 32 + (lane >> 4) * 8);
+        }
+    LaneStats<4 * FI, true> st;
+    if (STATS) st.init();
+
+    // DMA: lane = padded column, source column lane - 1 (columns 0 and W + 1.. stay zero)
+    const bool lane_ok = lane >= 1 && lane <= g.W;
+    const uint32_t lane_off = lane_ok ? (uint32_t)(lane - 1) * kRowBytes : 0x80000000u;
+    const uint32_t slot_lane = (uint32_t)wave * 1024u + (uint32_t)lane * 16u;
+    // the next row to load, R = cn * HP + cr
+    int cn = 0, cr = 0;
+    auto issue_rows = [&](int Ra, int Rb) {
+        for (int R = Ra; R <= Rb; ++R) {
+            const bool ok = cr >= 1 && cr <= g.H && cn < g.N;
+            const uint32_t row = (uint32_t)((cn * g.H + cr - 1) * g.W) * kRowBytes + (uint32_t)wave * 16u;
+            dma16(xr, smem + (R & (kRingRows - 1)) * kRingRowBytes + wave * 1024, ok ? row + lane_off : 0x80000000u, 0);
+            if (++cr == HP) {
+                cr = 0;
+                ++cn;
+            }
+        }
+    };
+    // XF: the rows just landed, R = xn * HP + xr_ (a second cursor one batch behind)
+    int xn = 0, xrr = 0;
+    auto rewrite_rows = [&](int Ra, int Rb) {
+        // this wave's chunk (channels 8 wave .. 8 wave + 7): scalar loads through the constant
+        // address space, so the 16 coefficients take no VGPRs between batches
+        typedef __attribute__((address_space(4))) const float* ConstF;
+        ConstF ab = (ConstF)g.in_ab;
+        float xa[8], xb[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            xa[j] = ab[8 * wave + j];
+            xb[j] = ab[g.Cin + 8 * wave + j];
+        }
+        const uint32_t base = lds_addr(smem) + slot_lane;
+        for (int R = Ra; R <= Rb; R += 4) {
+            uint32_t ad[4];
+            uint32_t keep = 0;
+            const int cnt = Rb - R + 1 < 4 ? Rb - R + 1 : 4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int Rj = j < cnt ? R + j : R;
+                ad[j] = base + (uint32_t)(Rj & (kRingRows - 1)) * kRingRowBytes;
+                if (j < cnt) {
+                    keep |= (uint32_t)(xrr >= 1 && xrr <= g.H && xn < g.N) << j;
+                    if (++xrr == HP) {
+                        xrr = 0;
+                        ++xn;
+                    }
+                }
+            }
+            bn_slots4(ad, cnt, lane_ok ? keep : 0u, xa, xb, g.in_lo);
+        }
+    };
+    // rows [lo, hi] that tile t reads
+    auto tile_rows = [&](int t, int& lo, int& hi) {
+        const int m0 = t * kBM;
+        const int ml = m0 + kBM - 1 < g.M ? m0 + kBM - 1 : g.M - 1;
+        const int n0 = m0 / OHW, oh0 = (m0 - n0 * OHW) / g.OW;
+        const int nl = ml / OHW, ohl = (ml - nl * OHW) / g.OW;
+        lo = n0 * HP + oh0;
+        hi = nl * HP + ohl + 2;
+    };
+
+    // this lane's output pixel offset in the tile per fragment: rows << 16 | cols
+    int dqr[FJ];
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+        const int d = wm * 64 + j * 16 + ring_px(lane & 15), q = d / g.OW;
+        dqr[j] = (q << 16) | (d - q * g.OW);
+    }
+    const uint32_t kq_off = (uint32_t)(lane >> 4) * 1024u;
+
+    int lo = 0, hi = -1, xa_lo = 0, xa_hi = -1;
+    if (t0 < t1) {
+        tile_rows(t0, lo, hi);
+        cn = lo / HP;
+        cr = lo - cn * HP;
+        xn = cn;
+        xrr = cr;
+        issue_rows(lo, hi);
+        xa_lo = lo;
+        xa_hi = hi;
+    }
+    for (int t = t0; t < t1; ++t) {
+        // tile t's rows landed; only the previous tile's epilogue stores (FI * FJ per lane) may still fly
+        if (t == t0) wait_vmcnt<0>();
+        else wait_vmcnt<FI * FJ>();
+        if (XF) {
+            rewrite_rows(xa_lo, xa_hi);
+            wait_lds_writes();
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const int lo_t = lo, hi_t = hi;
+        if (t + 1 < t1) {
+            int lo2, hi2;
+            tile_rows(t + 1, lo2, hi2);
+            issue_rows(hi_t + 1, hi2);
+            xa_lo = hi_t + 1;
+            xa_hi = hi2;
+            lo = lo2;
+            hi = hi2;
+        }
+        const int m0 = t * kBM;
+        const int n0 = m0 / OHW, r0m = m0 - n0 * OHW, oh0 = r0m / g.OW, ow0 = r0m - oh0 * g.OW;
+        uint32_t base[FJ][3];              // per fragment and kernel row kh
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+            int ow = ow0 + (dqr[j] & 0xFFFF), oh = oh0 + (dqr[j] >> 16), dn = 0;
+            if (ow >= g.OW) {
+                ow -= g.OW;
+                ++oh;
+            }
+            while (oh >= g.OH) {
+                oh -= g.OH;
+                ++dn;
+            }
+            int R = lo_t + dn * HP + oh - oh0;
+            if (m0 + (dqr[j] >> 16) * g.OW + (dqr[j] & 0xFFFF) >= g.M) {   // past M: a finite row, not stored
+                R = lo_t;
+                ow = 0;
+            }
+            const uint32_t col = (uint32_t)ow * 16u + kq_off;
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) base[j][kh] = (uint32_t)((R + kh) & (kRingRows - 1)) * kRingRowBytes + col;
+        }
+        (void)hi_t;
+        f32x4 acc[FJ][FI];
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+#pragma unroll
+            for (int i = 0; i < FI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int kh = tap / 3, kw = tap % 3;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                bf16x8 xf[FJ];
+#pragma unroll
+                for (int j = 0; j < FJ; ++j)
+                    xf[j] = *reinterpret_cast<const bf16x8*>(smem + base[j][kh] + kw * 16 + ks * 4096);
+#pragma unroll
+                for (int i = 0; i < FI; ++i)
+#pragma unroll
+                    for (int j = 0; j < FJ; ++j)
+                        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tap * 2 + ks][i], xf[j], acc[j][i], 0, 0, 0);
+            }
+        }
+        const bool full = m0 + kBM <= g.M, first = t == t0;
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+            const int m = m0 + wm * 64 + j * 16 + ring_px(lane & 15);
+            __bf16* dst = g.y + (size_t)(m < g.M ? m : 0) * 64 + wn * 32 + 4 * (lane >> 4);
+            if (full) store_fragment<FI, STATS, false>(acc[j], dst, true, first && j == 0, st);
+            else store_fragment<FI, STATS, true>(acc[j], dst, m < g.M, first && j == 0, st);
+        }
+    }
+    if (STATS) write_stats<4 * FI, 4, 64>(st, wn * 32, wm, reinterpret_cast<float*>(smem), g.stats,
+                                          (int)blockIdx.x, 64, 0);
+}
+
 // ---- 3x3 / stride 1 / pad 1 with Cin = 64 k >= 128 and Cout % 128 == 0 (ResNet layers 2-4):
 // halo tiles with streamed weights. conv_dma_kernel re-fetches each pixel once per tap (48 KB of
 // L2 traffic per 256 x 128 x 64 step); here a (pixel tile, 64-channel chunk cc) patch is DMA'd
@@ -1042,7 +1252,8 @@ __global__ __launch_bounds__(k1x1Threads) void conv1x1_kernel(const ConvGeom g) 
 // ---- launch plan: which kernel, its grid and the statistics rows (Gm x 3 x Cout floats)
 struct Plan {
     int kind = 0;          // 1: halo 64 -> 64, 2: dma 256 x 128, 3: dma 256 x 64, 4: halo, streamed
-                           // weights, 5: dma 512 x 128, 6: dma 256 x 256, 7: 1x1 streaming
+                           // weights, 5: dma 512 x 128, 6: dma 256 x 256, 7: 1x1 streaming,
+                           // 8: row-ring 64 -> 64
     int grid = 0;
     int parts = 0;         // statistics rows
     size_t lds = 0;
@@ -1089,6 +1300,27 @@ Plan make_plan(ConvGeom& g, int flags) {
     const int cus = cu_count();
     const int policy = tile_policy(flags);
     const bool halo_ok = policy != MCGMIL_CONV_TILE_NOHALO;
+    if (halo_ok && g.Cin == 64 && g.Cout == 64 && g.KH == 3 && g.KW == 3 && g.stride == 1 && g.pad == 1 &&
+        MCGMIL_C64_RING && g.W + 2 <= kRingCols) {
+        // the row ring holds the padded rows of two consecutive tiles: output rows 2 kBM pixels can
+        // span, + 2 halo rows, + 2 pad rows per image boundary crossed
+        const int rows = (2 * kBM - 1 + g.OW - 1) / g.OW + 1;
+        const int imgs = (2 * kBM - 1 + g.OH * g.OW - 1) / (g.OH * g.OW) + 1;
+        if (rows + 2 + 2 * (imgs - 1) <= kRingRows) {
+            HaloGeom hg{};
+            hg.WP = g.W + 2;
+            hg.tiles = g.tiles_m;
+            g.tiles_n = 1;
+            g.Gm = hg.tiles < cus ? hg.tiles : cus;
+            hg.g = g;
+            p.kind = 8;
+            p.grid = g.Gm;
+            p.parts = g.Gm;
+            p.lds = kRingBytes;
+            p.hg = hg;
+            return p;
+        }
+    }
     if (halo_ok && g.Cin == 64 && g.Cout == 64 && g.KH == 3 && g.KW == 3 && g.stride == 1 && g.pad == 1) {
         HaloGeom hg;
         hg.WP = g.W + 2;
@@ -1212,6 +1444,13 @@ int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
                                       : (xf ? conv3x3_halo_kernel<false, true> : conv3x3_halo_kernel<false, false>));
         return launch_lds(k, grid, block, p.lds, s, hg);
     }
+    if (p.kind == 8) {
+        HaloGeom hg = p.hg;
+        hg.g = g;
+        auto k = stats ? (xf ? conv3x3c64_ring_kernel<true, true> : conv3x3c64_ring_kernel<true, false>)
+                       : (xf ? conv3x3c64_ring_kernel<false, true> : conv3x3c64_ring_kernel<false, false>);
+        return launch_lds(k, grid, block, p.lds, s, hg);
+    }
     if (p.kind == 7) {
         const dim3 b1(k1x1Threads);
         auto k = stats ? conv1x1_kernel<2, true> : conv1x1_kernel<2, false>;     // Cin = 64
@@ -1305,7 +1544,7 @@ int mcgmil_conv_input_bn(const mcgmil_conv_args* a, int32_t* supported) {
     b.in_ab = reinterpret_cast<const float*>(16);   // a plan with the input BatchNorm
     ConvGeom g = geom_of(&b);
     const int kind = make_plan(g, a->flags).kind;
-    *supported = kind == 1 || kind == 4;
+    *supported = kind == 1 || kind == 4 || kind == 8;
     return MCGMIL_OK;
 }
 
@@ -1328,7 +1567,7 @@ int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream) {
     if ((uintptr_t)a->in_ab & 3u) return fail(MCGMIL_E_ALIGN, "in_ab must be 4-byte aligned");
     ConvGeom g = geom_of(a);
     const Plan p = make_plan(g, a->flags);
-    if (a->in_ab && p.kind != 1 && p.kind != 4)
+    if (a->in_ab && p.kind != 1 && p.kind != 4 && p.kind != 8)
         return fail(MCGMIL_E_UNSUPPORTED, "in_ab: this layer's kernel has no input BatchNorm "
                                           "(see mcgmil_conv_input_bn)");
     return launch(g, p, reinterpret_cast<hipStream_t>(stream));

@@ -34,6 +34,11 @@ SHAPES = [
     (3, 64, 30, 17, 64, 3, 1, 1),
     (2, 64, 20, 62, 64, 3, 1, 1),
     (1, 64, 5, 70, 64, 3, 1, 1),
+    # the row-ring 64 -> 64 kernel (conv3x3c64_ring_kernel, W + 2 <= 64 and two tiles' rows <= 16):
+    # more than 256 tiles, so a workgroup walks several tiles through the ring, an image boundary
+    # every ~4 tiles (20 x 50), and config 5's 56 x 56
+    (48, 64, 56, 56, 64, 3, 1, 1),
+    (120, 64, 20, 50, 64, 3, 1, 1),
     # 3x3 / stride 1 halo kernel with streamed weights (Cin >= 128): many small images per tile,
     # 3 input-channel chunks, 2 channel tiles, and a row too wide for the patch (generic kernel)
     (4, 128, 25, 20, 128, 3, 1, 1),
@@ -107,6 +112,33 @@ def test_conv2d_tile_policy_flags(cuda, shape):
         assert torch.all(err <= 2.0 ** -8 * ref.abs() + 1e-5 * mag), name
 
 
+RING_SHAPES = [(3, 64, 56, 56, 64), (48, 64, 56, 56, 64), (120, 64, 20, 50, 64), (2, 64, 20, 62, 64)]
+
+
+@pytest.mark.parametrize("shape", RING_SHAPES)
+def test_ring_kernel_bitwise_equals_generic(cuda, shape):
+    """The 64 -> 64 kernels accumulate each output over the same K steps in the same order (tap-major,
+    32 channels per MFMA), so the row-ring kernel (auto) is bitwise the generic LDS-DMA kernel
+    (MCGMIL_CONV_TILE_NOHALO), with and without an input BatchNorm."""
+    from mcgmil import _lib
+    from mcgmil.features import batchnorm_act, batchnorm_coefficients, conv2d
+    N, Cin, H, W, Cout = shape
+    conv = _layer(Cin, Cout, 3, 1, 1, cuda, 3 * Cin + W)
+    bn = _bn64(Cin, cuda, W)
+    g = torch.Generator(device=cuda).manual_seed(N + H * W)
+    x = (torch.randn(N, Cin, H, W, device=cuda, generator=g) * 1.5 + 0.2).bfloat16()
+    x = x.contiguous(memory_format=torch.channels_last)
+    nohalo = _lib.CONV_TILE_FLAGS["nohalo"]
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv2d(conv, x)
+        y_ref = conv2d(conv, x, flags=nohalo)
+        ab = batchnorm_coefficients(x, bn)
+        yb = conv2d(conv, x, in_ab=ab, in_relu=True)
+        yb_ref = conv2d(conv, batchnorm_act(x, bn, True), flags=nohalo)
+    assert torch.equal(y, y_ref)
+    assert torch.equal(yb, yb_ref)
+
+
 def test_conv2d_bf16_weights_and_repack(cuda):
     """A bf16 module runs without autocast; an in-place weight update is picked up (the packed
     weight cache is keyed by the tensor version)."""
@@ -171,6 +203,8 @@ def _bn64(C, dev, seed):
 # several channel tiles, and an input offset that makes mean >> std for the statistics
 STATS_SHAPES = [
     (3, 64, 56, 56, 64, 3, 1, 1, 0.0),
+    (40, 64, 56, 56, 64, 3, 1, 1, 1.0),
+    (120, 64, 20, 50, 64, 3, 1, 1, 0.0),
     (9, 64, 8, 6, 64, 3, 1, 1, 0.0),
     (2, 64, 28, 28, 128, 3, 2, 1, 0.0),
     (3, 128, 13, 11, 256, 3, 1, 1, 0.0),
@@ -246,6 +280,9 @@ def test_conv_statistics_deterministic(cuda, cin, cout, k, s, p):
 # tiles spanning several images, odd widths, ragged pixel counts, and an input offset
 INBN_SHAPES = [
     (3, 64, 56, 56, 64),
+    (48, 64, 56, 56, 64),
+    (120, 64, 20, 50, 64),
+    (2, 64, 20, 62, 64),
     (9, 64, 8, 6, 64),
     (3, 64, 30, 17, 64),
     (2, 64, 20, 60, 64),
@@ -296,9 +333,12 @@ def test_conv_input_bn_support_and_errors(cuda):
         assert not conv_input_bn(_layer(64, 128, 1, 1, 0, cuda, 1), x)        # 1 x 1
         x3 = torch.randn(2, 256, 14, 14, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
         assert not conv_input_bn(_layer(256, 256, 3, 1, 1, cuda, 1), x3)      # 14 x 14: 256 x 256 tiles
-        # width 62: the two patches fill the 160-KB LDS, no room for the a, b table
+        # width 62 runs the row ring (which takes in_ab); width 70 does not fit it, and the per-tile
+        # patch kernel's two patches then fill the 160-KB LDS, no room for the a, b table
         x62 = torch.randn(2, 64, 20, 62, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
-        assert not conv_input_bn(_layer(64, 64, 3, 1, 1, cuda, 1), x62)
+        assert conv_input_bn(_layer(64, 64, 3, 1, 1, cuda, 1), x62)
+        x70 = torch.randn(1, 64, 20, 70, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+        assert not conv_input_bn(_layer(64, 64, 3, 1, 1, cuda, 1), x70)
         ab = torch.zeros(2, 64, device=cuda)
         with pytest.raises(RuntimeError):
             conv2d(_layer(64, 128, 3, 2, 1, cuda, 1), x, in_ab=ab)
