@@ -474,6 +474,8 @@ struct HaloGeom {
     int NR;         // padded rows per patch (max over tiles)
     int patch_px;   // NR * WP rounded up to whole 8-pixel DMA pieces
     int tiles;
+    int q256, r256;   // ring kernel: kBM = q256 * OW + r256 (one tile's advance in output rows / columns)
+    int q255, r255;   // kBM - 1 (a tile's first pixel to its last)
 };
 
 // With XF (input BatchNorm) the [2][64] a, b table sits after the two patches; each lane rewrites
@@ -763,14 +765,29 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const Halo
             bn_slots4(ad, cnt, lane_ok ? keep : 0u, xa, xb, g.in_lo);
         }
     };
-    // rows [lo, hi] that tile t reads
-    auto tile_rows = [&](int t, int& lo, int& hi) {
-        const int m0 = t * kBM;
-        const int ml = m0 + kBM - 1 < g.M ? m0 + kBM - 1 : g.M - 1;
-        const int n0 = m0 / OHW, oh0 = (m0 - n0 * OHW) / g.OW;
-        const int nl = ml / OHW, ohl = (ml - nl * OHW) / g.OW;
-        lo = n0 * HP + oh0;
-        hi = nl * HP + ohl + 2;
+    // A tile's first pixel (n, oh, ow) advances by kBM = q256 rows + r256 columns: no division in
+    // the tile loop (the scalar unit's would be a long serial chain before the tile's barrier).
+    struct Px {
+        int n, oh, ow;
+    };
+    auto advance = [&](Px p, int q, int r) {
+        p.ow += r;
+        p.oh += q;
+        if (p.ow >= g.OW) {
+            p.ow -= g.OW;
+            ++p.oh;
+        }
+        while (p.oh >= g.OH) {
+            p.oh -= g.OH;
+            ++p.n;
+        }
+        return p;
+    };
+    // rows [lo, hi] that the tile starting at pixel f (index m0) reads
+    auto tile_rows = [&](Px f, int m0, int& lo, int& hi) {
+        const Px l = m0 + kBM - 1 < g.M ? advance(f, hg.q255, hg.r255) : Px{g.N - 1, g.OH - 1, g.OW - 1};
+        lo = f.n * HP + f.oh;
+        hi = l.n * HP + l.oh + 2;
     };
 
     // this lane's output pixel offset in the tile per fragment: rows << 16 | cols
@@ -783,8 +800,13 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const Halo
     const uint32_t kq_off = (uint32_t)(lane >> 4) * 1024u;
 
     int lo = 0, hi = -1, xa_lo = 0, xa_hi = -1;
+    Px f{0, 0, 0};                       // first pixel of tile t
     if (t0 < t1) {
-        tile_rows(t0, lo, hi);
+        const int m0 = t0 * kBM;
+        f.n = m0 / OHW;
+        f.oh = (m0 - f.n * OHW) / g.OW;
+        f.ow = m0 - f.n * OHW - f.oh * g.OW;
+        tile_rows(f, m0, lo, hi);
         cn = lo / HP;
         cr = lo - cn * HP;
         xn = cn;
@@ -804,21 +826,23 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const Halo
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const int lo_t = lo, hi_t = hi;
+        const Px ft = f;
+        const int m0 = t * kBM;
         if (t + 1 < t1) {
+            f = advance(f, hg.q256, hg.r256);
             int lo2, hi2;
-            tile_rows(t + 1, lo2, hi2);
+            tile_rows(f, m0 + kBM, lo2, hi2);
             issue_rows(hi_t + 1, hi2);
             xa_lo = hi_t + 1;
             xa_hi = hi2;
             lo = lo2;
             hi = hi2;
         }
-        const int m0 = t * kBM;
-        const int n0 = m0 / OHW, r0m = m0 - n0 * OHW, oh0 = r0m / g.OW, ow0 = r0m - oh0 * g.OW;
         uint32_t base[FJ][3];              // per fragment and kernel row kh
 #pragma unroll
         for (int j = 0; j < FJ; ++j) {
-            int ow = ow0 + (dqr[j] & 0xFFFF), oh = oh0 + (dqr[j] >> 16), dn = 0;
+            // pixels past M (last tile) read rows inside the ring and are not stored
+            int ow = ft.ow + (dqr[j] & 0xFFFF), oh = ft.oh + (dqr[j] >> 16), dn = 0;
             if (ow >= g.OW) {
                 ow -= g.OW;
                 ++oh;
@@ -827,11 +851,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const Halo
                 oh -= g.OH;
                 ++dn;
             }
-            int R = lo_t + dn * HP + oh - oh0;
-            if (m0 + (dqr[j] >> 16) * g.OW + (dqr[j] & 0xFFFF) >= g.M) {   // past M: a finite row, not stored
-                R = lo_t;
-                ow = 0;
-            }
+            const int R = lo_t + 2 * dn + oh + dn * g.OH - ft.oh;   // n HP + oh, relative to the tile's row
             const uint32_t col = (uint32_t)ow * 16u + kq_off;
 #pragma unroll
             for (int kh = 0; kh < 3; ++kh) base[j][kh] = (uint32_t)((R + kh) & (kRingRows - 1)) * kRingRowBytes + col;
@@ -1310,6 +1330,10 @@ Plan make_plan(ConvGeom& g, int flags) {
             HaloGeom hg{};
             hg.WP = g.W + 2;
             hg.tiles = g.tiles_m;
+            hg.q256 = kBM / g.OW;
+            hg.r256 = kBM % g.OW;
+            hg.q255 = (kBM - 1) / g.OW;
+            hg.r255 = (kBM - 1) % g.OW;
             g.tiles_n = 1;
             g.Gm = hg.tiles < cus ? hg.tiles : cus;
             hg.g = g;
