@@ -682,6 +682,16 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_kernel(const HaloGeom 
 //    kw * 16 + ks * 4 KiB: no address VALU in the tap loop.
 // The ring holds the rows of two consecutive tiles (the host checks the span <= 16): tile t + 1's
 // new rows load into ring rows tile t does not read, right after the barrier that opens tile t.
+#ifndef MCGMIL_RING_DIAG
+#define MCGMIL_RING_DIAG 0         // timing diagnostics only (wrong results): 1 no epilogue, 2 no row DMA
+#endif                             // after the first tile, 4 no barrier, 8 no wait for the row DMA,
+                                   // 16 contiguous DMA sources
+#ifndef MCGMIL_RING_WAVES
+#define MCGMIL_RING_WAVES 8        // 4: one wave per SIMD (128 x 32 wave tiles)
+#endif
+#ifndef MCGMIL_RING_PACK
+#define MCGMIL_RING_PACK true
+#endif
 #ifndef MCGMIL_C64_RING
 #define MCGMIL_C64_RING 1          // 0: conv3x3c64_kernel for layer 1 (A/B builds)
 #endif
@@ -691,10 +701,12 @@ constexpr int kRingRowBytes = 8 * kRingCols * 16;
 constexpr size_t kRingBytes = (size_t)kRingRows * kRingRowBytes;   // 128 KiB
 __device__ __forceinline__ int ring_px(int c) { return c < 4 ? c : c < 12 ? c + 4 : c - 8; }
 
-template <bool STATS, bool XF>
-__global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const HaloGeom hg) {
+template <bool STATS, bool XF, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void conv3x3c64_ring_kernel(const HaloGeom hg) {
     const ConvGeom& g = hg.g;
-    constexpr int FI = 2, FJ = 4, KSTEPS = 18;          // wave: 64 pixels x 32 channels
+    // NW = 8: two waves per SIMD, a wave 64 pixels x 32 channels; NW = 4: one wave per SIMD with the
+    // whole register file, a wave 128 pixels x 32 channels (FJ = 8)
+    constexpr int FI = 2, FJ = 32 / NW, KSTEPS = 18, PXG = 16 * FJ, CPW = 8 / NW;   // CPW: chunks per wave
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -712,20 +724,30 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const Halo
             const int co = wn * 32 + i * 16 + (lane & 15);
             wf[s][i] = *reinterpret_cast<const bf16x8*>(g.w + (size_t)co * 576 + s * 32 + (lane >> 4) * 8);
         }
-    LaneStats<4 * FI, true> st;
+    LaneStats<4 * FI, MCGMIL_RING_PACK> st;
     if (STATS) st.init();
 
     // DMA: lane = padded column, source column lane - 1 (columns 0 and W + 1.. stay zero)
     const bool lane_ok = lane >= 1 && lane <= g.W;
     const uint32_t lane_off = lane_ok ? (uint32_t)(lane - 1) * kRowBytes : 0x80000000u;
-    const uint32_t slot_lane = (uint32_t)wave * 1024u + (uint32_t)lane * 16u;
+    const uint32_t slot_lane = (uint32_t)lane * 16u;
     // the next row to load, R = cn * HP + cr
     int cn = 0, cr = 0;
     auto issue_rows = [&](int Ra, int Rb) {
         for (int R = Ra; R <= Rb; ++R) {
             const bool ok = cr >= 1 && cr <= g.H && cn < g.N;
-            const uint32_t row = (uint32_t)((cn * g.H + cr - 1) * g.W) * kRowBytes + (uint32_t)wave * 16u;
-            dma16(xr, smem + (R & (kRingRows - 1)) * kRingRowBytes + wave * 1024, ok ? row + lane_off : 0x80000000u, 0);
+            const uint32_t row = (uint32_t)((cn * g.H + cr - 1) * g.W) * kRowBytes;
+#pragma unroll
+            for (int q = 0; q < CPW; ++q) {     // chunk c = wave + NW q of the row
+                const int c = wave + NW * q;
+#if MCGMIL_RING_DIAG & 16   // timing only: each piece reads 1 KiB of contiguous source (wrong data)
+                dma16(xr, smem + (R & (kRingRows - 1)) * kRingRowBytes + c * 1024,
+                      ok ? row + (uint32_t)c * 1024u + (uint32_t)lane * 16u : 0x80000000u, 0);
+#else
+                dma16(xr, smem + (R & (kRingRows - 1)) * kRingRowBytes + c * 1024,
+                      ok ? row + (uint32_t)c * 16u + lane_off : 0x80000000u, 0);
+#endif
+            }
             if (++cr == HP) {
                 cr = 0;
                 ++cn;
@@ -739,13 +761,19 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const Halo
         // address space, so the 16 coefficients take no VGPRs between batches
         typedef __attribute__((address_space(4))) const float* ConstF;
         ConstF ab = (ConstF)g.in_ab;
+        int sn = xn, sr = xrr;
+#pragma unroll
+        for (int q = 0; q < CPW; ++q) {
+        const int c = wave + NW * q;
+        xn = sn;
+        xrr = sr;
         float xa[8], xb[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            xa[j] = ab[8 * wave + j];
-            xb[j] = ab[g.Cin + 8 * wave + j];
+            xa[j] = ab[8 * c + j];
+            xb[j] = ab[g.Cin + 8 * c + j];
         }
-        const uint32_t base = lds_addr(smem) + slot_lane;
+        const uint32_t base = lds_addr(smem) + slot_lane + (uint32_t)c * 1024u;
         for (int R = Ra; R <= Rb; R += 4) {
             uint32_t ad[4];
             uint32_t keep = 0;
@@ -763,6 +791,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const Halo
                 }
             }
             bn_slots4(ad, cnt, lane_ok ? keep : 0u, xa, xb, g.in_lo);
+        }
         }
     };
     // A tile's first pixel (n, oh, ow) advances by kBM = q256 rows + r256 columns: no division in
@@ -794,7 +823,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const Halo
     int dqr[FJ];
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
-        const int d = wm * 64 + j * 16 + ring_px(lane & 15), q = d / g.OW;
+        const int d = wm * PXG + j * 16 + ring_px(lane & 15), q = d / g.OW;
         dqr[j] = (q << 16) | (d - q * g.OW);
     }
     const uint32_t kq_off = (uint32_t)(lane >> 4) * 1024u;
@@ -818,12 +847,16 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const Halo
     for (int t = t0; t < t1; ++t) {
         // tile t's rows landed; only the previous tile's epilogue stores (FI * FJ per lane) may still fly
         if (t == t0) wait_vmcnt<0>();
+#if !(MCGMIL_RING_DIAG & 8)
         else wait_vmcnt<FI * FJ>();
+#endif
         if (XF) {
             rewrite_rows(xa_lo, xa_hi);
             wait_lds_writes();
         }
+#if !(MCGMIL_RING_DIAG & 4)
         __builtin_amdgcn_s_barrier();
+#endif
         asm volatile("" ::: "memory");
         const int lo_t = lo, hi_t = hi;
         const Px ft = f;
@@ -832,7 +865,9 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const Halo
             f = advance(f, hg.q256, hg.r256);
             int lo2, hi2;
             tile_rows(f, m0 + kBM, lo2, hi2);
+#if !(MCGMIL_RING_DIAG & 2)
             issue_rows(hi_t + 1, hi2);
+#endif
             xa_lo = hi_t + 1;
             xa_hi = hi2;
             lo = lo2;
@@ -879,15 +914,20 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3c64_ring_kernel(const Halo
             }
         }
         const bool full = m0 + kBM <= g.M, first = t == t0;
+#if MCGMIL_RING_DIAG & 1
+        // diagnostic (timing only): no epilogue
+        for (int j = 0; j < FJ; ++j) asm volatile("" ::"v"(acc[j][0]), "v"(acc[j][1]));
+        if (full) continue;
+#endif
 #pragma unroll
         for (int j = 0; j < FJ; ++j) {
-            const int m = m0 + wm * 64 + j * 16 + ring_px(lane & 15);
+            const int m = m0 + wm * PXG + j * 16 + ring_px(lane & 15);
             __bf16* dst = g.y + (size_t)(m < g.M ? m : 0) * 64 + wn * 32 + 4 * (lane >> 4);
             if (full) store_fragment<FI, STATS, false>(acc[j], dst, true, first && j == 0, st);
             else store_fragment<FI, STATS, true>(acc[j], dst, m < g.M, first && j == 0, st);
         }
     }
-    if (STATS) write_stats<4 * FI, 4, 64>(st, wn * 32, wm, reinterpret_cast<float*>(smem), g.stats,
+    if (STATS) write_stats<4 * FI, NW / 2, 64>(st, wn * 32, wm, reinterpret_cast<float*>(smem), g.stats,
                                           (int)blockIdx.x, 64, 0);
 }
 
@@ -1471,9 +1511,10 @@ int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
     if (p.kind == 8) {
         HaloGeom hg = p.hg;
         hg.g = g;
-        auto k = stats ? (xf ? conv3x3c64_ring_kernel<true, true> : conv3x3c64_ring_kernel<true, false>)
-                       : (xf ? conv3x3c64_ring_kernel<false, true> : conv3x3c64_ring_kernel<false, false>);
-        return launch_lds(k, grid, block, p.lds, s, hg);
+        constexpr int NW = MCGMIL_RING_WAVES;
+        auto k = stats ? (xf ? conv3x3c64_ring_kernel<true, true, NW> : conv3x3c64_ring_kernel<true, false, NW>)
+                       : (xf ? conv3x3c64_ring_kernel<false, true, NW> : conv3x3c64_ring_kernel<false, false, NW>);
+        return launch_lds(k, grid, dim3(NW * 64), p.lds, s, hg);
     }
     if (p.kind == 7) {
         const dim3 b1(k1x1Threads);
