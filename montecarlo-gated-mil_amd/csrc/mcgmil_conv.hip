@@ -985,8 +985,8 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
         const int r = 8 * (wave + 8 * j) + (lane >> 3);
         wrow[j] = ((uint32_t)(tn * BN + r) * K + (uint32_t)(((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
     }
-    auto issue_w = [&](int step, int buf) {     // step -> (tap, cc): K tile kt = tap * CC + cc
-        const int r = step % SPT, cc = r / 9, tap = r - cc * 9;
+    auto issue_w = [&](int r, int buf) {        // step r of a tile -> (tap, cc): K tile kt = tap * CC + cc
+        const int cc = r / 9, tap = r - cc * 9;
         const uint32_t soff = (uint32_t)(tap * CC + cc) * (kBK * 2u);
 #pragma unroll
         for (int j = 0; j < 2; ++j) dma16(wr, wst0 + buf * WSTAGE + (wave + 8 * j) * 1024, wrow[j], soff);
@@ -1001,10 +1001,26 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
     uint32_t okm = 0;                   // XF: bit k = piece k of the patch being loaded is in the image
     float xa[8], xb[8];                 // XF: a, b of this lane's chunk of that patch
     const int xchunk = (lane & 7) ^ ((4 * (wave & 1) + (lane >> 4)) & 7);
-    auto patch_begin = [&](int tm, int cc, int buf) {
-        const int m0 = tm * kBM;
-        pn = m0 / OHW;
-        prel = (m0 - pn * OHW) / g.OW + rr0;
+    // a tile's first pixel advances by kBM = q256 rows + r256 columns: no division per tile or patch
+    struct Px {
+        int n, oh, ow;
+    };
+    auto advance = [&](Px f) {
+        f.ow += hg.r256;
+        f.oh += hg.q256;
+        if (f.ow >= g.OW) {
+            f.ow -= g.OW;
+            ++f.oh;
+        }
+        while (f.oh >= g.OH) {
+            f.oh -= g.OH;
+            ++f.n;
+        }
+        return f;
+    };
+    auto patch_begin = [&](Px f, int cc, int buf) {
+        pn = f.n;
+        prel = f.oh + rr0;
         pcol = col0;
         while (prel >= HP) {
             prel -= HP;
@@ -1063,9 +1079,8 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
         dqr[j] = (q << 16) | (d - q * g.OW);
     }
     PatchPx pq[FJ];
-    auto tile_setup = [&](int tm) {
-        const int m0 = tm * kBM;
-        const int n0 = m0 / OHW, r0m = m0 - n0 * OHW, oh0 = r0m / g.OW, ow0 = r0m - oh0 * g.OW;
+    auto tile_setup = [&](Px f) {
+        const int oh0 = f.oh, ow0 = f.ow;
 #pragma unroll
         for (int j = 0; j < FJ; ++j) {
             int ow = ow0 + (dqr[j] & 0xFFFF), oh = oh0 + (dqr[j] >> 16), dn = 0;
@@ -1085,11 +1100,18 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
 
     if (steps <= 0) return;
     // prologue: the first (tile, cc) patch whole, the first weights
-    patch_begin(tm0, 0, 0);
+    Px fc;                              // first pixel of tile tm
+    {
+        const int m0 = tm0 * kBM;
+        fc.n = m0 / OHW;
+        fc.oh = (m0 - fc.n * OHW) / g.OW;
+        fc.ow = m0 - fc.n * OHW - fc.oh * g.OW;
+    }
+    patch_begin(fc, 0, 0);
 #pragma unroll
     for (int k = 0; k < 8; ++k) patch_piece(k);
     issue_w(0, 0);
-    tile_setup(tm0);
+    tile_setup(fc);
     int tm = tm0, r = 0, pbuf = 0;     // r = step within the tile
     int wait_kind = 0;                 // 0: vmcnt(0), 1: a patch piece after the weights, 2: stores
     for (int s = 0; s < steps; ++s) {
@@ -1109,13 +1131,13 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         wait_kind = 0;
-        if (s + 1 < steps) issue_w(s + 1, (s + 1) & 1);
+        if (s + 1 < steps) issue_w(r + 1 == SPT ? 0 : r + 1, (s + 1) & 1);
         // the next (tile, cc) patch: begun at tap 0, one piece per tap 0..7
         const bool more_patch = (r + 9 < SPT) || (tm + 1 < tm1);
         if (more_patch && tap < 8) {
             if (tap == 0) {
-                if (cc + 1 < CC) patch_begin(tm, cc + 1, pbuf ^ 1);
-                else patch_begin(tm + 1, 0, pbuf ^ 1);
+                if (cc + 1 < CC) patch_begin(fc, cc + 1, pbuf ^ 1);
+                else patch_begin(advance(fc), 0, pbuf ^ 1);
             }
             // vmcnt(1) at the next step leaves only this piece in flight; without a piece the
             // weights just issued must land: vmcnt(0)
@@ -1172,7 +1194,10 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
             wait_kind = 2;
             r = 0;
             ++tm;
-            if (tm < tm1) tile_setup(tm);
+            if (tm < tm1) {
+                fc = advance(fc);
+                tile_setup(fc);
+            }
         }
     }
     if (STATS) write_stats<4 * FI, WGM, BN>(st, wn * WN, wm, reinterpret_cast<float*>(smem), g.stats, gm,
@@ -1443,6 +1468,10 @@ Plan make_plan(ConvGeom& g, int flags) {
         hg.patch_px = hg.NR * hg.WP;
         if (hg.patch_px <= kPatchPx && (!g.in_ab || g.Cin <= 1024)) {
             hg.tiles = g.tiles_m;
+            hg.q256 = kBM / g.OW;
+            hg.r256 = kBM % g.OW;
+            hg.q255 = (kBM - 1) / g.OW;
+            hg.r255 = (kBM - 1) % g.OW;
             g.Gm = gm;
             hg.g = g;
             p.kind = 4;

@@ -1,4 +1,5 @@
-"""A/B of the ResNet layer-1 convolution (3x3, 64 -> 64, 56 x 56) across library builds
+"""A/B of a ResNet 3x3 / stride-1 block convolution (default layer 1: 64 -> 64 at 56 x 56; AB_CIN=128
+AB_HW=28 for layer 2) across library builds
 (scripts/build_variants.sh): every library named in AB_LIBS runs the three forms config 5 uses --
 plain, with the BatchNorm statistics epilogue, and with statistics + the input BatchNorm (in_ab) --
 on PROBE_K instances in its own process (MCGMIL_LIB), saves the outputs and reports the time per
@@ -24,19 +25,21 @@ def child(out_dir):
     K = int(os.environ.get("PROBE_K", "1507"))
     reps = int(os.environ.get("PROBE_REPS", "10"))
     lib = os.path.basename(os.environ["MCGMIL_LIB"])
+    C = int(os.environ.get("AB_CIN", "64"))
+    HW = int(os.environ.get("AB_HW", "56"))
     g = torch.Generator(device=dev).manual_seed(5)
-    conv = nn.Conv2d(64, 64, 3, 1, 1, bias=False).to(dev).eval()
-    bn = nn.BatchNorm2d(64)
+    conv = nn.Conv2d(C, C, 3, 1, 1, bias=False).to(dev).eval()
+    bn = nn.BatchNorm2d(C)
     deactivate_batchnorm(bn)
     bn = bn.to(dev).eval()
     with torch.no_grad():
         conv.weight.copy_(torch.randn(conv.weight.shape, device=dev, generator=g) * 0.06)
-        bn.weight.copy_(torch.randn(64, device=dev, generator=g) * 0.5 + 1.0)
-        bn.bias.copy_(torch.randn(64, device=dev, generator=g) * 0.3)
+        bn.weight.copy_(torch.randn(C, device=dev, generator=g) * 0.5 + 1.0)
+        bn.bias.copy_(torch.randn(C, device=dev, generator=g) * 0.3)
     conv = conv.to(memory_format=torch.channels_last)
-    x = (torch.randn(K, 64, 56, 56, device=dev, generator=g) + 0.3).bfloat16().contiguous(
+    x = (torch.randn(K, C, HW, HW, device=dev, generator=g) + 0.3).bfloat16().contiguous(
         memory_format=torch.channels_last)
-    flop = 2.0 * K * 56 * 56 * 64 * 64 * 9
+    flop = 2.0 * K * HW * HW * C * C * 9
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
         ab = batchnorm_coefficients(x, bn)
         forms = {"plain": lambda: conv2d(conv, x),
@@ -57,7 +60,7 @@ def child(out_dir):
             if part is not None:
                 tot = torch.stack([part[:, 0].sum(0), (part[:, 0] * part[:, 1]).sum(0)]).double().cpu()
                 torch.save(tot, os.path.join(out_dir, f"{name}_s.pt"))
-            print(json.dumps({"lib": lib, "form": name, "k": K, "ms": round(ms, 4),
+            print(json.dumps({"lib": lib, "form": name, "k": K, "cin": C, "hw": HW, "ms": round(ms, 4),
                               "tflops": round(flop / ms / 1e9, 1)}), flush=True)
 
 
