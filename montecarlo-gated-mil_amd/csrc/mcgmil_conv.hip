@@ -344,11 +344,23 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
             ohw[j] = (int)(((uint32_t)ih0 << 16) | ((uint32_t)iw0 & 0xFFFFu));
         }
     };
-    auto issue = [&](int step, int buf) {
-        const int tm = tm0 + step / g.KT, kt = step - (tm - tm0) * g.KT;
-        if (tm != itm) setup(tm);
-        const int khw = kt / g.cin_tiles, cc = kt - khw * g.cin_tiles;
-        const int kh = khw / g.KW, kw = khw - kh * g.KW;
+    // issue() is called for consecutive steps: its (tile, K tile) cursor advances by one per call --
+    // kt = (kh * KW + kw) * cin_tiles + cc -- without a runtime division per step
+    int i_tm = tm0, i_kt = 0, i_cc = 0, i_kw = 0, i_kh = 0;
+    auto issue = [&](int buf) {
+        if (i_tm != itm) setup(i_tm);
+        const int kt = i_kt, cc = i_cc, kh = i_kh, kw = i_kw;
+        if (++i_cc == g.cin_tiles) {
+            i_cc = 0;
+            if (++i_kw == g.KW) {
+                i_kw = 0;
+                ++i_kh;
+            }
+        }
+        if (++i_kt == g.KT) {
+            i_kt = i_cc = i_kw = i_kh = 0;
+            ++i_tm;
+        }
         const int koff = kh * g.W + kw;
         unsigned char* A = smem + buf * STAGE;
         unsigned char* B = A + BM * kRowBytes;
@@ -413,8 +425,8 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
 
     // NS LDS stages: step s + NS - 1 is issued into the stage step s - 1 used
     if (steps > 0) {
-        issue(0, 0);
-        if (NS == 3 && steps > 1) issue(1, 1);
+        issue(0);
+        if (NS == 3 && steps > 1) issue(1);
     }
     int buf = 0, kt = 0, tm = tm0;
     for (int s = 0; s < steps; ++s) {
@@ -423,7 +435,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (s + NS - 1 < steps) issue(s + NS - 1, buf == 0 ? NS - 1 : buf - 1);
+        if (s + NS - 1 < steps) issue(buf == 0 ? NS - 1 : buf - 1);
         compute(buf);
         buf = buf == NS - 1 ? 0 : buf + 1;
         if (++kt == g.KT) {

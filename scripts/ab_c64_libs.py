@@ -19,7 +19,7 @@ def child(out_dir):
     import torch
     import torch.nn as nn
     sys.path.insert(0, os.path.join(REPO, "montecarlo-gated-mil_amd"))
-    from mcgmil.features import batchnorm_coefficients, conv2d
+    from mcgmil.features import batchnorm_coefficients, conv2d, conv_input_bn
     from mcgmil.resnet import deactivate_batchnorm
     dev = torch.device("cuda", 0)
     K = int(os.environ.get("PROBE_K", "1507"))
@@ -43,8 +43,9 @@ def child(out_dir):
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
         ab = batchnorm_coefficients(x, bn)
         forms = {"plain": lambda: conv2d(conv, x),
-                 "stats": lambda: conv2d(conv, x, stats=True),
-                 "stats_inbn": lambda: conv2d(conv, x, stats=True, in_ab=ab, in_relu=True)}
+                 "stats": lambda: conv2d(conv, x, stats=True)}
+        if conv_input_bn(conv, x):      # the layer's kernel takes the input BatchNorm
+            forms["stats_inbn"] = lambda: conv2d(conv, x, stats=True, in_ab=ab, in_relu=True)
         for name, fn in forms.items():
             out = fn()
             torch.cuda.synchronize()
@@ -80,6 +81,8 @@ def main():
         dirs.append(d)
     ok = True
     for name in ("plain", "stats", "stats_inbn"):
+        if not os.path.exists(os.path.join(dirs[0], f"{name}_y.pt")):
+            continue
         ref = torch.load(os.path.join(dirs[0], f"{name}_y.pt"), weights_only=True)
         for d, lib in zip(dirs[1:], libs[1:]):
             y = torch.load(os.path.join(d, f"{name}_y.pt"), weights_only=True)

@@ -139,6 +139,32 @@ def test_ring_kernel_bitwise_equals_generic(cuda, shape):
     assert torch.equal(yb, yb_ref)
 
 
+def _ring_shapes(count, seed):
+    """Random 64 -> 64 shapes the row-ring kernel takes (W + 2 <= 64, two tiles' padded rows <= 16),
+    with more than 256 tiles (several per workgroup) in some."""
+    import random
+    rng = random.Random(seed)
+    out = []
+    while len(out) < count:
+        W = rng.randint(20, 62)
+        H = rng.randint(3, 40)
+        rows = (2 * 256 - 1 + W - 1) // W + 1
+        imgs = (2 * 256 - 1 + H * W - 1) // (H * W) + 1
+        if rows + 2 + 2 * (imgs - 1) > 16:
+            continue
+        many = len(out) % 2 == 0                     # > 256 tiles: workgroups walk the ring
+        N = (257 * 256) // (H * W) + 1 + rng.randint(0, 9) if many else rng.randint(1, 9)
+        out.append((N, 64, H, W, 64))
+    return out
+
+
+@pytest.mark.parametrize("shape", _ring_shapes(8, 5))
+def test_ring_kernel_random_shapes_bitwise(cuda, shape):
+    """Random geometries through the row ring (ragged last tiles, image boundaries inside tiles and
+    inside fragments, odd widths): bitwise the generic kernel, with and without the input BN."""
+    test_ring_kernel_bitwise_equals_generic(cuda, shape)
+
+
 def test_conv2d_bf16_weights_and_repack(cuda):
     """A bf16 module runs without autocast; an in-place weight update is picked up (the packed
     weight cache is keyed by the tensor version)."""
