@@ -116,7 +116,8 @@ int launch_row(const mcgmil::GateParams& gp, long long total_rows, hipStream_t s
 
 template <int MAXC, bool ONE>
 int launch_pp(const mcgmil::GateParams& gp0, long long total_rows, hipStream_t s) {
-    auto* k = &mcgmil::gate_pp_fused_kernel<__bf16, 8, 2, MAXC, ONE>;
+    auto* k = gp0.clock ? &mcgmil::gate_pp_fused_kernel<__bf16, 8, 2, MAXC, ONE, true>   // MCGMIL_CLOCK_PROBE
+                        : &mcgmil::gate_pp_fused_kernel<__bf16, 8, 2, MAXC, ONE>;
     if (int rc = raise_lds_limit(reinterpret_cast<const void*>(k), "gate_pp_fused_kernel LDS limit")) return rc;
     constexpr int cap = mcgmil::pp_fused_cap<MAXC>();
     mcgmil::GateParams gp = gp0;                 // t-groups per region for this kernel's cap

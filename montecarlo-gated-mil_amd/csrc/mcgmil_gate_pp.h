@@ -301,7 +301,7 @@ __host__ __device__ constexpr size_t pp_fused_lds_bytes() {
     return pp_lds_bytes<E, RT, MAXC>() + (size_t)2 * pp_fused_cap<MAXC>() * MAXC * 4 + 16 * 4 + 64;   // + Region
 }
 
-template <typename E, int RT, int PPW, int MAXC, bool ONE_CLASS>
+template <typename E, int RT, int PPW, int MAXC, bool ONE_CLASS, bool PROBE = false>
 __global__ __launch_bounds__(kPPThreads, 2) void gate_pp_fused_kernel(const GateParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int BM = 16 * RT;
@@ -314,6 +314,7 @@ __global__ __launch_bounds__(kPPThreads, 2) void gate_pp_fused_kernel(const Gate
     float* sred = szz + CAP * MAXC;                                               // [16]
     Region rg;
     if (!decode_region(p, (int)blockIdx.x, CAP, rg)) return;   // grid rounded up (ragged bags)
+    if constexpr (PROBE) clock_probe(p, 0);
     // As gate_fused_kernel: the region sits in LDS and the parameters are re-read from the
     // kernarg segment in every tile, so no scalar state stays live across the tile loop.
     Region* srg = reinterpret_cast<Region*>(sred + 16);
@@ -345,6 +346,7 @@ __global__ __launch_bounds__(kPPThreads, 2) void gate_pp_fused_kernel(const Gate
         float* Yo = p.Y + ((size_t)rg.bag * p.T + rg.t0 + j) * p.C;
         softmax_group(threadIdx.x, true, rg.Nb, p.C, lgj, zzj, Ao, Yo, sred);
     }
+    if constexpr (PROBE) clock_probe(p, 1);
 }
 
 }  // namespace mcgmil

@@ -108,7 +108,7 @@ def test_pp_fused_kernel_fits(fused_asm):
     # loop and reloaded once per 128-row tile outside the K loop (12 bytes of frame) -- more would mean
     # spills in the tile code itself
     syms = set(re.findall(r"\.set (_ZN6mcgmil20gate_pp_fused_kernel\w*)\.private_seg_size", fused_asm))
-    assert len(syms) == 4, syms       # MAXC in {2, 4} x one class per wave or not
+    assert len(syms) == 8, syms       # MAXC in {2, 4} x one class per wave or not x clock probe
     for sym in syms:
         assert kernel_meta(fused_asm, sym, "private_seg_size") <= 16, sym
         assert kernel_meta(fused_asm, sym, "num_vgpr") + kernel_meta(fused_asm, sym, "num_agpr") <= 256, sym

@@ -396,7 +396,7 @@ def test_random_shapes_fused_two_kernel_oracle(cuda, case):
         assert np.abs(A[b].numpy().reshape(T, C, n) - Ar).max() <= tol["A"] * max(np.abs(Ar).max(), 1e-30)
 
 
-@pytest.mark.parametrize("path,shared", [("fused", False), ("two_kernel", False), ("two_kernel", True)])
+@pytest.mark.parametrize("path,shared", [("fused", False), ("fused", True), ("two_kernel", False), ("two_kernel", True)])
 def test_clock_probe(cuda, path, shared):
     """MCGMIL_CLOCK_PROBE (the clock bench.py states in every roofline): the probed launch runs the
     PROBE instantiation of the same tile kernel -- outputs bitwise equal to the unprobed launch --
