@@ -172,6 +172,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the fp32 reference-precision and single-bag lines")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-calibration", action="store_true",
+                    help="skip the MFMA ceiling calibration (roofline.measured_peak_tflops)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ:
@@ -191,7 +193,13 @@ def main():
 
     if args.workload == "cfg5":
         import bench_cfg5
-        out = bench_cfg5.run(args, world, rank, dev, PEAK_TFLOPS["bf16"])
+        from mcgmil import _lib
+        _lib.load()
+        if not args.no_calibration:
+            CALIB["bf16" if args.features == "bf16" else "f32"] = \
+                mfma_calibration(dev, "bf16" if args.features == "bf16" else "f32")
+        out = bench_cfg5.run(args, world, rank, dev, PEAK_TFLOPS["bf16"],
+                             calib=lambda a, dt: vs_measured(a, dt))
         if rank == 0:
             print(json.dumps(out))
         if world > 1:
@@ -202,6 +210,8 @@ def main():
 
     _lib.load()
     if args.workload == "single":
+        if not args.no_calibration:
+            CALIB["bf16"] = mfma_calibration(dev, "bf16")
         out = single_bag_line(args, dev)
         print(json.dumps(out))
         return 0
@@ -227,6 +237,11 @@ def main():
     r = measure_batch(sizes, ids, T, args.dtype, bool(args.shared), dev, world, args.steps,
                       args.warmup, busy_s=args.busy_seconds, gather=True, seed_rank=rank)
     el, gate_ms, fused, nreg, nbytes_packed = r["el"], r["gate_ms"], r["fused"], r["regions"], r["packed_bytes"]
+    # the box's own MFMA ceiling, measured right after the headline's timed steps (chip under load)
+    if not args.no_calibration:
+        CALIB["bf16"] = mfma_calibration(dev, "bf16")
+        if world == 1 and args.workload == "cfg3" and not args.no_secondary:
+            CALIB["f32"] = mfma_calibration(dev, "f32")
     esize = 2 if args.dtype == "bf16" else 4
     total_bag_samples = total_bags * T * args.steps
     value = total_bag_samples / el
@@ -275,7 +290,7 @@ def main():
                          # pooling) when fused, the gate GEMM kernel alone otherwise
                          "timed_path": "fused: gate+softmax+pooling" if fused else "two-kernel: gate only",
                          "kernel_ms": gate_ms, "algorithmic_tflop_per_launch": F / 1e12,
-                         **at_clock(achieved, PEAK_TFLOPS[args.dtype], r["clock"])},
+                         **at_clock(achieved, PEAK_TFLOPS[args.dtype], r["clock"], args.dtype)},
             "roofline_hbm": {"achieved": hbm_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": hbm_gbs / PEAK_HBM_GBS,
                              "algorithmic_bytes_per_launch": hbm_bytes},
@@ -286,6 +301,7 @@ def main():
                 "value": total_bag_samples / r["cold"][0], "ms_per_step": r["cold"][0] * 1e3 / args.steps,
                 "kernel_ms": r["cold"][1],
                 "frac": F / (r["cold"][1] * 1e-3) / 1e12 / PEAK_TFLOPS[args.dtype]},
+            "mfma_calibration": {k: v for k, v in CALIB.items()},
             "shared_heads": shared_line,
             "fp32_reference_precision": fp32_line,
             "single_bag": single,
@@ -432,15 +448,90 @@ def measure_batch(sizes, ids, T, dtype, shared, dev, world, steps, warmup, busy_
             "clock": clock}
 
 
-def at_clock(achieved, peak, clock):
+def at_clock(achieved, peak, clock, dtype="bf16"):
     """The roofline's clock keys: the shader clock the launch ran at and the fraction of the peak
-    scaled to that clock (the spec peak assumes MAX_CLOCK_MHZ)."""
+    scaled to that clock (the spec peak assumes MAX_CLOCK_MHZ), plus the fractions of the box's
+    measured MFMA ceiling (vs_measured)."""
     if clock is None:
-        return {"clock_mhz": None, "frac_at_clock": None}
+        return {"clock_mhz": None, "frac_at_clock": None, **vs_measured(achieved, dtype)}
     return {"clock_mhz": round(clock["median"], 1), "clock_mhz_p10_p90": [round(clock["p10"], 1), round(clock["p90"], 1)],
             "frac_at_clock": achieved / (peak * clock["median"] / MAX_CLOCK_MHZ),
             "clock_source": f"in-kernel s_memtime/s_memrealtime x 100 MHz, median of {clock['workgroups']} "
-                            f"workgroups of one probed launch right after the timed steps"}
+                            f"workgroups of one probed launch right after the timed steps",
+            **vs_measured(achieved, dtype, clock["median"])}
+
+
+def mfma_calibration(dev, dtype, warm_s=2.0, timed_s=1.0, launch_ms=20.0):
+    """The MFMA rate this box sustains (include/mcgmil_calib.h): a bare loop at the gate kernels'
+    occupancy (one 512-thread workgroup per CU, two waves per SIMD), B fragments re-read from LDS
+    by ds_read_b128 each step, random full-range operands. >= warm_s seconds of back-to-back
+    launches first (the chip settles its clock under load, MI355X_MICROARCH.md 'DVFS give-back'
+    item 6), then timed_s seconds timed by HIP events on the launch stream, then one launch
+    clock-probed (s_memtime / s_memrealtime per workgroup)."""
+    from mcgmil import _lib, ops
+    lib = _lib.load()
+    code = _lib.MCGMIL_BF16 if dtype == "bf16" else _lib.MCGMIL_F32
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    sink = torch.empty(cus * 512, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    fps = lib.mcgmil_mfma_calib_flops_per_step(code)
+
+    def launch(steps, seed=1, rec=None):
+        _lib.check(lib.mcgmil_mfma_calib(code, cus, steps, seed, ctypes.c_void_p(sink.data_ptr()),
+                                         None if rec is None else ctypes.c_void_p(rec.data_ptr()), sh),
+                   "mfma_calib")
+    # size one launch to ~launch_ms from a short probe
+    launch(200)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    launch(2000)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    steps = max(100, int(2000 * launch_ms / max(e0.elapsed_time(e1), 1e-3)))
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < warm_s:
+        for i in range(10):
+            launch(steps, seed=i + 2)
+        torch.cuda.synchronize()
+    n = max(5, int(timed_s * 1e3 / launch_ms))
+    e0.record(stream)
+    for i in range(n):
+        launch(steps, seed=100 + i)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    rec = ops.clock_record(dev)
+    launch(steps, seed=7, rec=rec)
+    torch.cuda.synchronize()
+    clock = ops.clock_mhz(rec)
+    tflops = fps * cus * steps / (ms * 1e-3) / 1e12
+    return {"tflops": tflops, "clock_mhz": None if clock is None else round(clock["median"], 1),
+            "launch_ms": ms, "launches_timed": n, "warm_s": round(time.perf_counter() - t0, 2),
+            "workgroups": cus, "steps_per_launch": steps,
+            "loop": ("v_mfma_f32_16x16x32_bf16 x 32 per wave-step" if dtype == "bf16"
+                     else "v_mfma_f32_16x16x4_f32 x 128 per wave-step") +
+                    ", 2 waves/SIMD, B via ds_read_b128 from LDS, random operands in [-1, 1)"}
+
+
+CALIB = {}      # dtype -> mfma_calibration() of this process (bench.py fills it once per run)
+
+
+def vs_measured(achieved, dtype, clock_mhz=None):
+    """Roofline keys against the box's measured MFMA ceiling: frac_of_measured = achieved / the
+    calibration loop's TFLOP/s (both wall rates on this GPU, this process); with the kernel's own
+    clock, per_clock_frac_of_measured = (achieved / its clock) / (calibration / its clock)."""
+    c = CALIB.get(dtype)
+    if not c:
+        return {"measured_peak_tflops": None, "frac_of_measured": None}
+    out = {"measured_peak_tflops": round(c["tflops"], 1), "measured_peak_clock_mhz": c["clock_mhz"],
+           "frac_of_measured": achieved / c["tflops"],
+           "measured_peak_source": "mcgmil_mfma_calib (include/mcgmil_calib.h), same process, "
+                                   f"{c['warm_s']} s of back-to-back launches before timing"}
+    if clock_mhz and c["clock_mhz"]:
+        out["per_clock_frac_of_measured"] = (achieved / clock_mhz) / (c["tflops"] / c["clock_mhz"])
+    return out
 
 
 def shared_secondary(args, dev, steps=10, warmup=3):
@@ -483,7 +574,46 @@ def fp32_secondary(args, dev, bags=64, steps=10, warmup=2):
                                     else "gate_pipe_kernel (fp32 MFMA 16x16x4)"),
                          "timed_path": "fused: gate+softmax+pooling" if r["fused"] else "two-kernel: gate only",
                          "algorithmic_tflop_per_launch": F / 1e12,
-                         **at_clock(ach, PEAK_TFLOPS["f32"], r["clock"])}}
+                         **at_clock(ach, PEAK_TFLOPS["f32"], r["clock"], "f32")}}
+
+
+def _single_bag_entry(m, dev, N, T, L, D, C):
+    g = torch.Generator(device=dev).manual_seed(7)
+    H = torch.randn(N, L, device=dev, generator=g).abs_().bfloat16()
+    call = lambda i: m.mc_inference_features(H, T=T, seed=100 + i, return_stats=True)  # noqa: E731
+    for i in range(5):
+        call(i)
+    torch.cuda.synchronize()
+    reps = 50
+    # host time per call, nothing queued
+    t0 = time.perf_counter()
+    for i in range(reps):
+        call(i)
+    host = (time.perf_counter() - t0) / reps
+    torch.cuda.synchronize()
+    # device time per call: a busy kernel queued ahead (~0.1 s), so the host enqueues every
+    # call before the GPU reaches them
+    torch.cuda._sleep(int(2e8))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s = torch.cuda.current_stream(dev)
+    e0.record(s)
+    for i in range(reps):
+        call(i)
+    e1.record(s)
+    torch.cuda.synchronize()
+    gpu = e0.elapsed_time(e1) / reps
+    lat = []
+    for i in range(10):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        call(i)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
+    F = flops_per_bag(N, T, L, D, C, C)
+    ach = F / (gpu * 1e-3) / 1e12
+    return {"gpu_ms": gpu, "host_ms": host * 1e3, "sync_ms": sorted(lat)[len(lat) // 2] * 1e3,
+            "achieved_tflops": ach, "frac": ach / PEAK_TFLOPS["bf16"],
+            "bag_samples_per_s": T / (gpu * 1e-3), **vs_measured(ach, "bf16")}
 
 
 def single_bag_line(args, dev, quiet=False):
@@ -503,46 +633,16 @@ def single_bag_line(args, dev, quiet=False):
     m.load_state_dict({k: torch.from_numpy(v).reshape(own[k].shape) for k, v in sd.items()}, strict=False)
     m.compute_dtype = torch.bfloat16
     m = m.to(dev).eval()
-    res = {}
-    for N in (args.n, 1507):
-        g = torch.Generator(device=dev).manual_seed(7)
-        H = torch.randn(N, L, device=dev, generator=g).abs_().bfloat16()
-        call = lambda i: m.mc_inference_features(H, T=T, seed=100 + i, return_stats=True)  # noqa: E731
-        for i in range(5):
-            call(i)
-        torch.cuda.synchronize()
-        reps = 50
-        # host time per call, nothing queued
-        t0 = time.perf_counter()
-        for i in range(reps):
-            call(i)
-        host = (time.perf_counter() - t0) / reps
-        torch.cuda.synchronize()
-        # device time per call: a busy kernel queued ahead (~0.1 s), so the host enqueues every
-        # call before the GPU reaches them
-        torch.cuda._sleep(int(2e8))
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s = torch.cuda.current_stream(dev)
-        e0.record(s)
-        for i in range(reps):
-            call(i)
-        e1.record(s)
-        torch.cuda.synchronize()
-        gpu = e0.elapsed_time(e1) / reps
-        lat = []
-        for i in range(10):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            call(i)
-            torch.cuda.synchronize()
-            lat.append(time.perf_counter() - t0)
-        F = flops_per_bag(N, T, L, D, C, C)
-        ach = F / (gpu * 1e-3) / 1e12
-        res[f"N{N}"] = {"gpu_ms": gpu, "host_ms": host * 1e3, "sync_ms": sorted(lat)[len(lat) // 2] * 1e3,
-                        "achieved_tflops": ach, "frac": ach / PEAK_TFLOPS["bf16"],
-                        "bag_samples_per_s": T / (gpu * 1e-3)}
+    by_t = {}
+    # the headline's T and the reference caller's own sample count (infer.py:191 passes
+    # N=config['N'], config.yml:12 sets 50)
+    for T in dict.fromkeys((args.T, 50)):
+        res = by_t[T] = {}
+        for N in (args.n, 1507):
+            res[f"N{N}"] = _single_bag_entry(m, dev, N, T, L, D, C)
     out = {"metric": "one bag per call (infer.py:187-191): head device time per bag",
-           "unit": "ms", "dtype": "bf16", "T": T, "bags": res,
+           "unit": "ms", "dtype": "bf16", "T": args.T, "bags": by_t[args.T],
+           **{f"T{t}": {"T": t, "bags": r} for t, r in by_t.items() if t != args.T},
            "path": "MultiHeadGatedAttentionMIL.mc_inference_features -> mcgmil_mcdo_forward "
                    "(two-kernel path + bag statistics)"}
     return out

@@ -7,9 +7,9 @@ separate attention) -> softmax probabilities -> attention-map mean/std over pass
 grid (infer.py:187-219 without the plotting).
 
 Two precisions (--features):
-  fp32  the reference's precision end to end: fp32 instances, the build's fp32 MFMA block
-        convolutions (mcgmil_conv2d_f32: fp32 operands and accumulation) and fused BN kernels, the
-        stem convolution (3 input channels) on MIOpen, fp32 head operands;
+  fp32  the reference's precision end to end: fp32 instances, the build's fp32 MFMA convolutions
+        (mcgmil_conv2d_f32, conv32_kernel: fp32 operands and accumulation; the 3-channel stem in its
+        gather mode, features.py) and fused BN kernels, fp32 head operands;
   bf16  bf16 instances, the build's HIP backbone under autocast, bf16 head operands. The run
         also pushes its last image through the fp32 pipeline (same seed, untimed) and reports
         the drift of prob_mean / A_mean / Y against it.
@@ -32,7 +32,8 @@ import torch.distributed as dist
 RESNET18_GFLOP = 3.64          # per 3 x 224 x 224 instance (2 x 1.82 GMAC)
 # MI355X fp32 peak, vector = matrix (no xf32 on gfx950): 157.3 TFLOP/s spec, MI355X_MICROARCH.md
 # spec table. The fp32 line's dominant stage is the ResNet: this build's fp32 MFMA convolutions
-# (v_mfma_f32_16x16x4_f32) for the blocks, MIOpen for the 3-channel stem.
+# (conv32_kernel, v_mfma_f32_16x16x4_f32) for the blocks and, in gather mode, the 3-channel stem
+# (profiles/r03/conv32_bnfold/kernel_stats_cfg5_fp32.csv: no MIOpen kernel in the trace).
 PEAK_FP32_TFLOPS = 157.3
 H_IMG, W_IMG, PS, OVERLAP, THRESH = 7036, 2800, 224, 0.75, 0.75   # config.yml:31,34
 BLOB = (0.30, 0.58)     # semi-axes of the breast region (fractions of H, W): k = 1,507 tiles kept
@@ -95,7 +96,7 @@ def cpu_baseline(k, T, budget_s=20.0):
                       f"scaled); torch {torch.__version__} CPU, {threads} threads"}
 
 
-def run(args, world, rank, dev, peak_tflops):
+def run(args, world, rank, dev, peak_tflops, calib=None):
     from mcgmil import MultiHeadGatedAttentionMIL, deactivate_batchnorm
     from mcgmil.infer import mc_predict_image
     from mcgmil.patcher import ImagePatcher
@@ -175,7 +176,7 @@ def run(args, world, rank, dev, peak_tflops):
                                f"T={T} -> attention map mean/std",
                    "images_per_s": images / el, "instances_per_bag": k, "T": T,
                    "features": ("bf16: HIP backbone (autocast), bf16 head operands" if bf16 else
-                                "fp32: fp32 MFMA block convolutions + fused BN (HIP), stem convolution on MIOpen, fp32 head operands"),
+                                "fp32: fp32 MFMA convolutions incl. the gather-mode stem + fused BN (HIP, conv32_kernel), fp32 head operands"),
                    "drift_vs_fp32_pipeline": drift,
                    "stage_ms": stage_ms, "parallelism": f"one image per GPU per step, {world} GPU(s)"},
         "roofline": {"bound": "mfma", "achieved": feat_tflops,
@@ -183,8 +184,9 @@ def run(args, world, rank, dev, peak_tflops):
                      "frac": feat_tflops / (peak_tflops if bf16 else PEAK_FP32_TFLOPS), "traffic": None,
                      "kernel": "ResNet-18 feature extractor (the dominant stage): " +
                                ("stem + implicit-GEMM convolutions + fused BN (HIP, bf16)" if bf16 else
-                                "fp32 MFMA block convolutions + fused BN (HIP, fp32); stem convolution on MIOpen"),
-                     "algorithmic_tflop_per_launch": k * RESNET18_GFLOP / 1e3},
+                                "fp32 MFMA convolutions (conv32_kernel, the stem in gather mode) + fused BN (HIP, fp32)"),
+                     "algorithmic_tflop_per_launch": k * RESNET18_GFLOP / 1e3,
+                     **(calib(feat_tflops, "bf16" if bf16 else "f32") if calib else {})},
         "cpu_baseline": cpu,
     }
 

@@ -47,9 +47,10 @@
 extern "C" {
 #endif
 
-#define MCGMIL_ABI_VERSION 4   /* 2: mcgmil_args.flags (path selection); 3: mcgmil_conv_args.flags,
-                                  mcgmil_stem_args.flags (mcgmil_features.h); 4: MCGMIL_GATE_ROW and
-                                  the row-gate weight stream in the packed weights, MCGMIL_CLOCK_PROBE */
+#define MCGMIL_ABI_VERSION 5   /* 2: mcgmil_args.flags (path selection); 3: mcgmil_conv_args.flags,
+                                  mcgmil_stem_args.flags (mcgmil_features.h); 4: MCGMIL_CLOCK_PROBE (and a
+                                  row-gate flag); 5: the row-gate flag (3 << 2) and its weight stream in the
+                                  packed weights removed -- measured slower everywhere, DESIGN.md §5 */
 
 enum mcgmil_status {
     MCGMIL_OK = 0,
@@ -64,27 +65,33 @@ enum mcgmil_dtype { MCGMIL_F32 = 0, MCGMIL_BF16 = 1 };
 
 /* mcgmil_args.flags: which launch path mcgmil_gate_softmax_pool / mcgmil_mcdo_forward take. All
  * paths give bitwise the same A and Y (tests/test_gpu_fused.py); the choice is performance only.
- * The environment variables MCGMIL_FUSED (0 | 1 | auto) and MCGMIL_GATE (pipe | pp | row), when
+ * The environment variables MCGMIL_FUSED (0 | 1 | auto) and MCGMIL_GATE (pipe | pp), when
  * set, override the flags (A/B timing of an unmodified caller); they are read once per process. */
 enum mcgmil_flags {
     MCGMIL_PATH_AUTO = 0,        /* fused launch for bf16 batches of equal-size bags with >= 16,384
-                                    regions, else the two kernels */
-    MCGMIL_PATH_FUSED = 1,       /* the fused launch whenever it applies (bf16 or fp32, L % 64 == 0,
-                                    <= 16 gate tile pairs, no replay masks) */
+                                    regions whose heads run gate_pipe_kernel (separate heads), else
+                                    the two kernels */
+    MCGMIL_PATH_FUSED = 1,       /* the fused launch (gate_fused_kernel) whenever it applies: bf16 or
+                                    fp32, L % 64 == 0, L >= 128, the tile within 160 KiB of LDS
+                                    (bf16: L <= 1024), <= 16 gate tile pairs, no replay masks, gate
+                                    not forced to MCGMIL_GATE_PP */
     MCGMIL_PATH_TWO_KERNEL = 2,  /* never fused: gate scores -> workspace -> softmax/pooling */
     MCGMIL_PATH_MASK = 3,
     MCGMIL_GATE_AUTO = 0 << 2,   /* two-kernel path, bf16 heads: gate_pipe_kernel for > 8 gate tile
                                     pairs (separate heads), gate_pp_kernel for <= 8 (shared) */
     MCGMIL_GATE_PIPE = 1 << 2,   /* always gate_pipe_kernel (one 8-wave workgroup per CU) */
-    MCGMIL_GATE_PP = 2 << 2,     /* gate_pp_kernel (two 4-wave workgroups per CU) where it applies */
-    MCGMIL_GATE_ROW = 3 << 2,    /* rowgate_scores_kernel (one wave per SIMD, each wave owns whole
-                                    rows; bf16, D % 32 == 0, <= 16 gate column blocks of 32) */
+    MCGMIL_GATE_PP = 2 << 2,     /* gate_pp_kernel (two 4-wave workgroups per CU) where it applies;
+                                    3 << 2 is invalid since ABI 5 */
     MCGMIL_GATE_MASK = 3 << 2,
     MCGMIL_CLOCK_PROBE = 1 << 4  /* measurement: the gate launch's workgroups 0..MCGMIL_CLOCK_SLOTS-1
                                     write their (s_memtime, s_memrealtime) at start and end into
                                     args->debug ([MCGMIL_CLOCK_SLOTS][4] uint64, required): the shader
                                     clock the launch ran at = d(memtime) / d(realtime) x 100 MHz.
-                                    Outputs are unchanged; no stamp executes without the flag */
+                                    Outputs are unchanged; no stamp executes without the flag.
+                                    Stamped launches: gate_fused_kernel, gate_pipe_kernel and
+                                    gate_pp_kernel with their own Philox masks; the replay-mask,
+                                    generic (gate_scores_kernel) and softmax/statistics kernels write
+                                    no record, so a record stays all zero when only they ran */
 };
 #define MCGMIL_CLOCK_SLOTS 1024
 

@@ -14,7 +14,6 @@
 #include "mcgmil_kernels.h"
 #include "mcgmil_gate_pp.h"
 #include "mcgmil_fused.h"
-#include "mcgmil_rowgate.h"
 
 namespace mcgmil_detail {
 
@@ -103,7 +102,7 @@ int validate_batch(const mcgmil_args* a) {
     if (!(a->p_feat >= 0.f && a->p_feat <= 1.f) || !(a->p_att >= 0.f && a->p_att <= 1.f))
         return fail(MCGMIL_E_INVALID, "dropout probabilities must be in [0, 1]");
     if ((a->flags & ~(MCGMIL_PATH_MASK | MCGMIL_GATE_MASK | MCGMIL_CLOCK_PROBE)) != 0 ||
-        (a->flags & MCGMIL_PATH_MASK) == 3 || a->reserved != 0)
+        (a->flags & MCGMIL_PATH_MASK) == 3 || (a->flags & MCGMIL_GATE_MASK) == (3 << 2) || a->reserved != 0)
         return fail(MCGMIL_E_INVALID, "flags must be MCGMIL_PATH_* | MCGMIL_GATE_* [| MCGMIL_CLOCK_PROBE] and reserved 0");
     if ((a->flags & MCGMIL_CLOCK_PROBE) && !a->debug)
         return fail(MCGMIL_E_INVALID, "MCGMIL_CLOCK_PROBE needs args->debug ([MCGMIL_CLOCK_SLOTS][4] uint64)");
@@ -118,18 +117,10 @@ struct Layout {
 // Smallest row tile any gate kernel uses (sizes the tile plan).
 constexpr int kMinBM = 16;
 
-// The 16x16x32 operand tiles of gate_pipe/pp/scores_kernel, then (bf16, D % 32 == 0) the
-// row-gate weight stream and classifier table (mcgmil_rowgate.h), 256-byte aligned.
-size_t packed_tiles_bytes(const mcgmil_args* a) {
+// The 16x16x32 operand tiles of gate_pipe/pp/scores_kernel.
+size_t packed_bytes_for(const mcgmil_args* a) {
     const size_t P = (size_t)a->G * (a->D / 16);
     return (2 * P + 1) * (size_t)(a->L / 32) * 512 * elem_size(a->h_dtype);
-}
-size_t packed_rowgate_bytes(const mcgmil_args* a) {
-    return a->h_dtype == MCGMIL_BF16 ? mcgmil::rg_packed_bytes(a->L, a->G, a->D) : 0;
-}
-size_t packed_bytes_for(const mcgmil_args* a) {
-    const size_t r = packed_rowgate_bytes(a);
-    return r ? align_up(packed_tiles_bytes(a), 256) + r : packed_tiles_bytes(a);
 }
 
 Layout layout_for(const mcgmil_args* a) {
@@ -225,12 +216,11 @@ int launch_gate_pp(const mcgmil::GateParams& gp, hipStream_t s) {
 #ifndef MCGMIL_GATE_DEFAULT
 #define MCGMIL_GATE_DEFAULT 0       // A/B builds: 1 pipe, 2 pp
 #endif
-int gate_mode(int flags) {   // 0 auto, 1 pipe, 2 pp, 3 row
+int gate_mode(int flags) {   // 0 auto, 1 pipe, 2 pp
     static const int env = [] {
         const char* e = getenv("MCGMIL_GATE");
         if (e && strcmp(e, "pipe") == 0) return 1;
         if (e && strcmp(e, "pp") == 0) return 2;
-        if (e && strcmp(e, "row") == 0) return 3;
         return -1;
     }();
     if (env >= 0) return env;
@@ -259,70 +249,11 @@ int dispatch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
                : launch_gate_pipe<E, PPW, MAXC, false, false>(gp, s);
 }
 
-// Row-owner gate kernels (mcgmil_rowgate.h): bf16, gate columns in 4, 8 or 16 blocks of 32.
-int device_cus() {
-    static std::mutex mu;
-    static int cache[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    std::lock_guard<std::mutex> lock(mu);
-    if (!cache[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cache[dev] = n;
-    }
-    return cache[dev];
-}
-
-// The reference's heads: C = 2 classes, D = 128, shared (G = 1) or separate (G = 2) gates; L a
-// multiple of 64 of at least 128 (K steps of 16 in groups of 4 ring slots, four peeled at each end
-// of a tile).
-bool rowgate_applies(const mcgmil::GateParams& gp) {
-    return gp.Wr && gp.D == 128 && (gp.G == 1 || gp.G == 2) && gp.L % 64 == 0 && gp.L >= 128 && gp.C <= 4;
-}
-
-// The LDS-DMA weight stream (asm operand reads) wherever the kernel fits without spills; the
-// replayed-mask separate-heads kernel with 4 classes stages the weights through registers
-// (tests/test_codegen_guard.py checks both). MCGMIL_RG_SAFE_ALL (timing builds): staging everywhere.
-template <int G, int MAXC, bool REPLAY>
-constexpr bool rowgate_dma() {
-#ifdef MCGMIL_RG_SAFE_ALL
-    return false;
-#else
-    return !(REPLAY && G == 2 && MAXC == 4);
-#endif
-}
-
-template <int G, int DB, int MAXC, bool REPLAY>
-int launch_rowgate(const mcgmil::GateParams& gp, hipStream_t s) {
-    constexpr int NCB = 2 * G * DB;
-    auto* k = &mcgmil::rowgate_scores_kernel<G, DB, MAXC, REPLAY, rowgate_dma<G, MAXC, REPLAY>()>;
-    if (int rc = mcgmil_detail::raise_lds_limit(reinterpret_cast<const void*>(k), "rowgate_scores_kernel LDS limit"))
-        return rc;
-    const long long tiles = (gp.total_samples + mcgmil::kRgRows - 1) / mcgmil::kRgRows;
-    if (tiles == 0) return MCGMIL_OK;
-    if (gp.uniform_rows <= 0)
-        if (int rc = launch_plan(gp, mcgmil::kRgRows, s)) return rc;
-    const long long grid = tiles < device_cus() ? tiles : device_cus();
-    const size_t lds = mcgmil::rg_lds_bytes<NCB, MAXC>(gp.L, gp.G, gp.C, gp.D);
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(mcgmil::kRgThreads), lds, s, gp, tiles);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "rowgate_scores_kernel launch");
-}
-
-template <int MAXC>
-int dispatch_rowgate(const mcgmil::GateParams& gp, hipStream_t s) {
-    const bool replay = gp.keep_feat != nullptr;
-    if (gp.G == 2) return replay ? launch_rowgate<2, 4, MAXC, true>(gp, s) : launch_rowgate<2, 4, MAXC, false>(gp, s);
-    return replay ? launch_rowgate<1, 4, MAXC, true>(gp, s) : launch_rowgate<1, 4, MAXC, false>(gp, s);
-}
-
 template <typename E, int MAXC>
 int dispatch_gate_maxc(const mcgmil::GateParams& gp, int L, int dtype, int flags, hipStream_t s) {
     const bool pipe_ok = L % 64 == 0;          // the pipelined K loop is unrolled by two steps
     if constexpr (sizeof(E) == 2) {
         const int mode = gate_mode(flags);
-        if (mode == 3 && rowgate_applies(gp)) return dispatch_rowgate<MAXC>(gp, s);
         if (pipe_ok && mode != 1) {
             if (gp.P <= 2 * mcgmil::kPPWaves) return dispatch_gate_pp<8, 2, MAXC>(gp, s);
             if (mode == 2 && gp.P <= 4 * mcgmil::kPPWaves) return dispatch_gate_pp<4, 4, MAXC>(gp, s);
@@ -375,41 +306,34 @@ int try_fused_maxc(const mcgmil::GateParams& gp, long long total_rows, int L, in
     *rc = MCGMIL_OK;
     // (L >= 128: the fused pipeline peels two K steps at each end of a tile)
     if (gp.keep_feat) return 0;
-    bool row = false, pp = false;
-    if constexpr (sizeof(E) == 2) {       // bf16: the kernel dispatch_gate_maxc would pick
+    bool pipe_heads = true;               // the heads the two-kernel path runs on gate_pipe_kernel
+    if constexpr (sizeof(E) == 2) {
         const int mode = gate_mode(flags);
-        row = mode == 3 && rowgate_applies(gp) &&
-              mcgmil::rg_fused_lds_bytes<2 * 2 * 4, MAXC>(L, gp.G, gp.C, gp.D) <= 160 * 1024;
-        const bool pipe = mode == 1 || (mode == 0 && gp.P > 2 * mcgmil::kPPWaves);
-        // gate_pp_kernel's heads (<= 8 gate tile pairs: shared heads) fuse on its own tile
-        pp = !row && !pipe && gp.P <= 2 * mcgmil::kPPWaves && L % 64 == 0 && L >= 128;
-        if (!row && !pipe && !pp) return 0;
+        if (mode == 2) return 0;          // MCGMIL_GATE_PP: gate_pp_kernel has no single-launch form
+        pipe_heads = mode == 1 || gp.P > 2 * mcgmil::kPPWaves;
     }
-    if (!row && !pp && (L % 64 != 0 || L < 128 || gp.P > 2 * mcgmil::kGateWaves)) return 0;
-    if (!row && !pp && mcgmil::fused_kernel_lds_bytes<E, MAXC>(L) > 160 * 1024) return 0;   // bf16 L > 1024
+    if (L % 64 != 0 || L < 128 || gp.P > 2 * mcgmil::kGateWaves) return 0;
+    if (mcgmil::fused_kernel_lds_bytes<E, MAXC>(L) > 160 * 1024) return 0;   // bf16 L > 1024
     const int fm = fused_mode(flags);
     if (fm == 0) return 0;
-    const int cap = pp ? mcgmil::pp_fused_cap<MAXC>() : mcgmil::fused_cap<MAXC>();
+    constexpr int cap = mcgmil::fused_cap<MAXC>();
     // auto: bf16 uniform batches only -- on ragged ones (config 4) the fused launch measured 2.8%
     // slower (regions of 16-32 tiles straddling t-groups; profiles/r03/bench_cfg4*.log), and in fp32
-    // (which spills in the tile loop) 13-18% slower (profiles/r03/probe_fused_f32.log)
-    // gate_pp_fused_kernel: opt-in only -- 16.68 vs 16.56 ms for the two-kernel path on 256 shared-head
-    // bags of config 3 (profiles/r05/pp_fused_probe.log)
-    if (fm < 0 && (pp || sizeof(E) != 2 || gp.uniform_rows <= 0 ||
+    // (which spills in the tile loop) 13-18% slower (profiles/r03/probe_fused_f32.log). bf16 shared
+    // heads keep gate_pp_kernel + softmax_pool_kernel: the 8-wave tile in one launch measured 5.53
+    // vs 4.04-4.10 ms per 64 bags (profiles/r05/fused_ab_*), and a fused form of gate_pp_kernel's own
+    // tile 16.68 vs 16.56 ms per 256 bags (profiles/r05/pp_fused_probe.log; removed in round 6).
+    if (fm < 0 && (!pipe_heads || sizeof(E) != 2 || gp.uniform_rows <= 0 ||
                    mcgmil_detail::fused_regions(gp, total_rows, cap, true) < kFusedMinRegions))
         return 0;
     // same kernel shape as dispatch_gate_pipe: one class per wave for separate heads
-    const int ppw = pp ? 2 : gp.P <= mcgmil::kGateWaves ? 1 : 2;   // (gate_pp: dispatch_gate_pp<8, 2>)
+    const int ppw = gp.P <= mcgmil::kGateWaves ? 1 : 2;
     const bool one = gp.G > 1 && gp.G == gp.C && (gp.D / 16) % ppw == 0;
     if (regions) {
-        mcgmil::GateParams g2 = gp;
-        if (pp) g2.region_t = gp.uniform_rows > 0 ? mcgmil::region_t_groups(gp.uniform_rows, gp.T, cap) : 0;
-        *regions = mcgmil_detail::fused_regions(g2, total_rows, cap, false);
+        *regions = mcgmil_detail::fused_regions(gp, total_rows, cap, false);
         return 1;
     }
-    *rc = row  ? mcgmil_detail::launch_rowgate_fused(gp, MAXC, total_rows, s)
-          : pp ? mcgmil_detail::launch_pp_fused(gp, MAXC, one, total_rows, s)
-               : mcgmil_detail::launch_gate_fused(gp, sizeof(E) == 2, ppw, MAXC, one, total_rows, s);
+    *rc = mcgmil_detail::launch_gate_fused(gp, sizeof(E) == 2, ppw, MAXC, one, total_rows, s);
     return 1;
 }
 
@@ -457,11 +381,6 @@ int mcgmil_pack_weights(const mcgmil_args* a, void* packed, void* stream) {
     if (a->h_dtype == MCGMIL_BF16) {
         hipLaunchKernelGGL(mcgmil::pack_weights_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, a->Wv,
                            a->Wu, a->wk, a->L, a->D, a->C, P, reinterpret_cast<__bf16*>(packed));
-        if (packed_rowgate_bytes(a))
-            hipLaunchKernelGGL(mcgmil::pack_rowgate_kernel<__bf16>, dim3(1024), dim3(256), 0, s, a->Wv, a->Wu,
-                               a->wk, a->L, a->D, a->G, a->C,
-                               reinterpret_cast<__bf16*>(static_cast<char*>(packed) +
-                                                         align_up(packed_tiles_bytes(a), 256)));
     } else
         hipLaunchKernelGGL(mcgmil::pack_weights_kernel<float>, dim3(blocks), dim3(256), 0, s, a->Wv,
                            a->Wu, a->wk, a->L, a->D, a->C, P, reinterpret_cast<float*>(packed));
@@ -503,9 +422,7 @@ int gate_params(const mcgmil_args* a, mcgmil::GateParams& gp) {
     gp.P = a->G * (a->D / 16);
     gp.total_samples = (long long)a->T * a->total_rows;
     gp.Wp = packed_ptr(a);
-    gp.wp_bytes = (uint32_t)packed_tiles_bytes(a);
-    gp.Wr = packed_rowgate_bytes(a) ? static_cast<const char*>(packed_ptr(a)) + align_up(packed_tiles_bytes(a), 256)
-                                    : nullptr;
+    gp.wp_bytes = (uint32_t)packed_bytes_for(a);
     gp.bv = a->bv;
     gp.bu = a->bu;
     gp.wa = a->wa;

@@ -5,8 +5,6 @@
 #define MCGMIL_KERNELS_TEMPLATES_ONLY   // the plain kernels live in mcgmil.hip's object
 #include "../../include/mcgmil.h"
 #include "mcgmil_kernels.h"
-#include "mcgmil_rowgate.h"
-#include "mcgmil_gate_pp.h"
 #include "mcgmil_error.h"
 #include "mcgmil_fused.h"
 
@@ -86,69 +84,7 @@ int launch_maxc(const mcgmil::GateParams& gp, int ppw, bool one, long long total
     return one ? launch<E, 2, MAXC, true>(gp, total_rows, s) : launch<E, 2, MAXC, false>(gp, total_rows, s);
 }
 
-template <int G, int MAXC>
-int launch_row(const mcgmil::GateParams& gp, long long total_rows, hipStream_t s) {
-    constexpr int NCB = 2 * G * 4;
-    auto* k = &mcgmil::rowgate_fused_kernel<G, 4, MAXC,
-#ifdef MCGMIL_RG_SAFE_ALL
-                                          false
-#else
-                                          true
-#endif
-                                          >;   // LDS-DMA where it fits without spills
-    if (int rc = raise_lds_limit(reinterpret_cast<const void*>(k), "rowgate_fused_kernel LDS limit")) return rc;
-    constexpr int cap = mcgmil::rg_fused_cap<MAXC>();
-    if (gp.uniform_rows <= 0) {
-        hipLaunchKernelGGL(mcgmil::plan_regions_kernel, dim3(1), dim3(1024), 0, s, gp.bag_off, gp.B,
-                           gp.T, cap, const_cast<int32_t*>(gp.region_off));
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return hip_fail(e, "plan_regions_kernel launch");
-    }
-    const long long grid = fused_regions(gp, total_rows, cap, false);
-    if (grid == 0) return MCGMIL_OK;
-    if (grid > 0x7fffffffll) return fail(MCGMIL_E_UNSUPPORTED, "too many regions for one launch");
-    const size_t lds = mcgmil::rg_fused_lds_bytes<NCB, MAXC>(gp.L, gp.G, gp.C, gp.D);
-    if (lds > 160 * 1024) return fail(MCGMIL_E_UNSUPPORTED, "row-gate fused kernel: L too large for its LDS");
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(mcgmil::kRgThreads), lds, s, gp);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "rowgate_fused_kernel launch");
-}
-
-template <int MAXC, bool ONE>
-int launch_pp(const mcgmil::GateParams& gp0, long long total_rows, hipStream_t s) {
-    auto* k = gp0.clock ? &mcgmil::gate_pp_fused_kernel<__bf16, 8, 2, MAXC, ONE, true>   // MCGMIL_CLOCK_PROBE
-                        : &mcgmil::gate_pp_fused_kernel<__bf16, 8, 2, MAXC, ONE>;
-    if (int rc = raise_lds_limit(reinterpret_cast<const void*>(k), "gate_pp_fused_kernel LDS limit")) return rc;
-    constexpr int cap = mcgmil::pp_fused_cap<MAXC>();
-    mcgmil::GateParams gp = gp0;                 // t-groups per region for this kernel's cap
-    gp.region_t = gp.uniform_rows > 0 ? mcgmil::region_t_groups(gp.uniform_rows, gp.T, cap) : 0;
-    if (gp.uniform_rows <= 0) {
-        hipLaunchKernelGGL(mcgmil::plan_regions_kernel, dim3(1), dim3(1024), 0, s, gp.bag_off, gp.B,
-                           gp.T, cap, const_cast<int32_t*>(gp.region_off));
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return hip_fail(e, "plan_regions_kernel launch");
-    }
-    const long long grid = fused_regions(gp, total_rows, cap, false);
-    if (grid == 0) return MCGMIL_OK;
-    if (grid > 0x7fffffffll) return fail(MCGMIL_E_UNSUPPORTED, "too many regions for one launch");
-    constexpr size_t lds = mcgmil::pp_fused_lds_bytes<__bf16, 8, MAXC>();
-    static_assert(lds <= 80 * 1024, "two workgroups per CU");
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(mcgmil::kPPThreads), lds, s, gp);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_pp_fused_kernel launch");
-}
-
 }  // namespace
-
-int launch_pp_fused(const mcgmil::GateParams& gp, int maxc, bool one, long long total_rows, hipStream_t s) {
-    if (maxc == 2) return one ? launch_pp<2, true>(gp, total_rows, s) : launch_pp<2, false>(gp, total_rows, s);
-    return one ? launch_pp<4, true>(gp, total_rows, s) : launch_pp<4, false>(gp, total_rows, s);
-}
-
-int launch_rowgate_fused(const mcgmil::GateParams& gp, int maxc, long long total_rows, hipStream_t s) {
-    if (gp.G == 2) return maxc == 2 ? launch_row<2, 2>(gp, total_rows, s) : launch_row<2, 4>(gp, total_rows, s);
-    return maxc == 2 ? launch_row<1, 2>(gp, total_rows, s) : launch_row<1, 4>(gp, total_rows, s);
-}
 
 int launch_gate_fused(const mcgmil::GateParams& gp, bool bf16, int ppw, int maxc, bool one,
                       long long total_rows, hipStream_t s) {

@@ -51,7 +51,7 @@ __host__ __device__ constexpr size_t pp_lds_bytes() {
 
 // One BM-row tile of the flattened (bag, t, n) space, rows R0 .. R0 + BM - 1, whose row table is
 // in `rinfo` (visible: the caller's barrier). Scores go to lg_out / z_out at row R0 + r - obase.
-// The body of gate_pp_kernel and, tile by tile over a region, of gate_pp_fused_kernel.
+// The body of gate_pp_kernel.
 template <typename E, int RT, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS>
 __device__ __forceinline__ void pp_tile(const GateParams& p, long long R0, unsigned char* smem, const int* rinfo,
                                         float* lg_out, float* z_out, long long obase) {
@@ -283,69 +283,6 @@ __global__ __launch_bounds__(kPPThreads, 2) void gate_pp_kernel(const GateParams
     __syncthreads();
     MCGMIL_STAMP(p, 1);
     pp_tile<E, RT, PPW, MAXC, REPLAY, ONE_CLASS>(p, R0, smem, rinfo, p.logits, p.zz, 0);
-    if constexpr (PROBE) clock_probe(p, 1);
-}
-
-// ---------------------------------------------------------------------------------------
-// gate_pp_fused_kernel -- the shared-heads hot path in ONE launch (model.py:280-316), on
-// gate_pp_kernel's tile: 4-wave workgroups, two per CU, each owning a region (t-groups [t0, t1)
-// of one bag, decode_region with the cap below) whose 128-row tiles run through pp_tile with the
-// logits and classifier projections kept in LDS, then softmax_group per t-group. Bags of more
-// than the cap keep one t-group per region and go through the global workspace. Same tile code
-// and same softmax_group as gate_pp_kernel + softmax_pool_kernel: A and Y bitwise the same.
-// ---------------------------------------------------------------------------------------
-template <int MAXC>
-__host__ __device__ constexpr int pp_fused_cap() { return MAXC <= 2 ? 2048 : 512; }   // 2 workgroups / CU
-template <typename E, int RT, int MAXC>
-__host__ __device__ constexpr size_t pp_fused_lds_bytes() {
-    return pp_lds_bytes<E, RT, MAXC>() + (size_t)2 * pp_fused_cap<MAXC>() * MAXC * 4 + 16 * 4 + 64;   // + Region
-}
-
-template <typename E, int RT, int PPW, int MAXC, bool ONE_CLASS, bool PROBE = false>
-__global__ __launch_bounds__(kPPThreads, 2) void gate_pp_fused_kernel(const GateParams p) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int BM = 16 * RT;
-    static_assert(BM == kPipeBM, "regions are planned in 128-row tiles");
-    constexpr int CAP = pp_fused_cap<MAXC>();
-    int* rinfo = reinterpret_cast<int*>(smem + (size_t)2 * RT * 64 * 8 * sizeof(E) +
-                                        ((size_t)kPPWaves * MAXC * 4 * BM + (size_t)MAXC * BM) * 4);
-    float* slg = reinterpret_cast<float*>(smem + pp_lds_bytes<E, RT, MAXC>());   // [CAP][C]
-    float* szz = slg + CAP * MAXC;                                                // [CAP][C]
-    float* sred = szz + CAP * MAXC;                                               // [16]
-    Region rg;
-    if (!decode_region(p, (int)blockIdx.x, CAP, rg)) return;   // grid rounded up (ragged bags)
-    if constexpr (PROBE) clock_probe(p, 0);
-    // As gate_fused_kernel: the region sits in LDS and the parameters are re-read from the
-    // kernarg segment in every tile, so no scalar state stays live across the tile loop.
-    Region* srg = reinterpret_cast<Region*>(sred + 16);
-    if (threadIdx.x == 0) *srg = rg;
-    const int ntiles = rg.ntiles;
-    for (int i = 0; i < ntiles; ++i) {
-        __syncthreads();                 // the previous tile's row table and staging slots are free
-        Region* qr = srg;
-        asm volatile("" : "+v"(qr));
-        const GateParams pt = reload_kernarg_params(p);
-        const Region r = *qr;
-        const long long R0 = r.S + (long long)region_tile(r, i) * BM;
-        fill_row_table_region<BM>(pt, r, R0, rinfo);
-        __syncthreads();
-        const bool lds = r.Nb <= CAP;
-        pp_tile<E, RT, PPW, MAXC, false, ONE_CLASS>(pt, R0, smem, rinfo, lds ? slg : pt.logits, lds ? szz : pt.zz,
-                                                lds ? r.S : 0);
-    }
-    __syncthreads();
-    rg = *srg;
-    const bool in_lds = rg.Nb <= CAP;
-    // softmax + pooling per t-group (model.py:305-316)
-    const int ng = rg.t1 - rg.t0;
-    for (int j = 0; j < ng; ++j) {
-        const long long row0 = (long long)j * rg.Nb;
-        const float* lgj = in_lds ? slg + row0 * p.C : p.logits + (rg.S + row0) * p.C;
-        const float* zzj = in_lds ? szz + row0 * p.C : p.zz + (rg.S + row0) * p.C;
-        float* Ao = p.A ? p.A + (size_t)p.T * p.C * rg.ob + (size_t)(rg.t0 + j) * p.C * rg.Nb : nullptr;
-        float* Yo = p.Y + ((size_t)rg.bag * p.T + rg.t0 + j) * p.C;
-        softmax_group(threadIdx.x, true, rg.Nb, p.C, lgj, zzj, Ao, Yo, sred);
-    }
     if constexpr (PROBE) clock_probe(p, 1);
 }
 

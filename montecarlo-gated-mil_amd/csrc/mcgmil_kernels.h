@@ -26,7 +26,6 @@ struct GateParams {
     long long total_samples;       // T * total_rows
     const void* Wp;                // packed weights (see pack_weights_kernel)
     uint32_t wp_bytes;             // their size (buffer-descriptor range)
-    const void* Wr;                // the row-gate weight stream (mcgmil_rowgate.h) or nullptr
     const float* bv;
     const float* bu;
     const float* wa;

@@ -12,10 +12,10 @@ CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(os.path.dirname(ROOT), "include")
 LIB = os.path.join(PKG, "libmcgmil.so")
 SOURCES = ["mcgmil.hip", "mcgmil_fused.hip", "mcgmil_image.hip", "mcgmil_bn.hip", "mcgmil_conv.hip", "mcgmil_stem.hip",
-           "mcgmil_conv32.hip"]
+           "mcgmil_conv32.hip", "mcgmil_calib.hip"]
 DEPS = ["mcgmil.hip", "mcgmil_fused.hip", "mcgmil_fused.h", "mcgmil_image.hip", "mcgmil_bn.hip", "mcgmil_conv.hip", "mcgmil_stem.hip",
-        "mcgmil_conv32.hip", "mcgmil_kernels.h",
-        "mcgmil_device.h", "mcgmil_error.h", "mcgmil_gate_pp.h", "mcgmil_rowgate.h"]
+        "mcgmil_conv32.hip", "mcgmil_calib.hip", "mcgmil_kernels.h",
+        "mcgmil_device.h", "mcgmil_error.h", "mcgmil_gate_pp.h"]
 ARCH = os.environ.get("MCGMIL_OFFLOAD_ARCH", "gfx950")
 # No packed-fp32 VALU (v_pk_fma/mul/add_f32): with ROCm 7.2's compiler a packed write into the
 # source VGPR of a just-issued v_rcp_f32 / v_exp_f32 gets no wait states, and on gfx950 the
@@ -37,7 +37,7 @@ def _stale(out: str = LIB) -> bool:
     if os.path.getmtime(os.path.abspath(__file__)) > t:      # build flags changed
         return True
     deps = [os.path.join(CSRC, d) for d in DEPS] + \
-        [os.path.join(INCLUDE, h) for h in ("mcgmil.h", "mcgmil_image.h", "mcgmil_features.h")]
+        [os.path.join(INCLUDE, h) for h in ("mcgmil.h", "mcgmil_image.h", "mcgmil_features.h", "mcgmil_calib.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 

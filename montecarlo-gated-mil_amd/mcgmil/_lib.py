@@ -18,13 +18,13 @@ MCGMIL_BF16 = 1
 MCGMIL_U8 = 2
 MCGMIL_U16 = 3
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 # mcgmil_args.flags (include/mcgmil.h enum mcgmil_flags)
 PATH_FLAGS = {"auto": 0, "fused": 1, "two_kernel": 2}
 # mcgmil_conv_args.flags / mcgmil_stem_args.flags (include/mcgmil_features.h)
 CONV_TILE_FLAGS = {"auto": 0, "nohalo": 1, "small": 2, "big512": 3}
 STEM_POOL_UNSPLIT = 1
-GATE_FLAGS = {"auto": 0, "pipe": 1 << 2, "pp": 2 << 2, "row": 3 << 2}
+GATE_FLAGS = {"auto": 0, "pipe": 1 << 2, "pp": 2 << 2}
 CLOCK_PROBE = 1 << 4         # MCGMIL_CLOCK_PROBE: clock record of the gate launch into args.debug
 CLOCK_SLOTS = 1024           # MCGMIL_CLOCK_SLOTS: [slots][4] uint64
 
@@ -44,6 +44,8 @@ EXPORTED = (
     "mcgmil_conv_stats_parts_f32",
     "mcgmil_stem_args_size", "mcgmil_stem_packed_size", "mcgmil_pack_stem_weights",
     "mcgmil_stem_workspace_size", "mcgmil_stem_forward",
+    # include/mcgmil_calib.h (measurement)
+    "mcgmil_mfma_calib_flops_per_step", "mcgmil_mfma_calib",
 )
 
 _vp = ctypes.c_void_p
@@ -235,6 +237,10 @@ def bind(path: str, mcdo_only: bool = False, any_abi: bool = False):
     L.mcgmil_pack_stem_weights.restype = ctypes.c_int
     L.mcgmil_stem_forward.argtypes = [ps, _vp]
     L.mcgmil_stem_forward.restype = ctypes.c_int
+    L.mcgmil_mfma_calib_flops_per_step.argtypes = [ctypes.c_int]
+    L.mcgmil_mfma_calib_flops_per_step.restype = ctypes.c_int64
+    L.mcgmil_mfma_calib.argtypes = [ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _vp, _vp, _vp]
+    L.mcgmil_mfma_calib.restype = ctypes.c_int
     if L.mcgmil_stem_args_size() != ctypes.sizeof(StemArgs):
         raise MCGMILError(f"ABI mismatch: sizeof(mcgmil_stem_args)={L.mcgmil_stem_args_size()} "
                           f"but the ctypes mirror is {ctypes.sizeof(StemArgs)} bytes")

@@ -45,6 +45,14 @@ class AuxiliaryLoss(nn.Module):
         raise ValueError(f"Unknown loss type: {self.loss_type}")
 
 
+def _walk(root, path):
+    """root._modules[path[0]]._modules[path[1]]... (KeyError if a link is gone)."""
+    m = root
+    for k in path:
+        m = m._modules[k]
+    return m
+
+
 def _draw_seed() -> int:
     # key for the Philox stream, taken from torch's default CPU generator
     return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
@@ -88,20 +96,38 @@ class MultiHeadGatedAttentionMIL(nn.Module):
             return [self.attention_V[0]], [self.attention_U[0]]
         return [m[0] for m in self.attention_V], [m[0] for m in self.attention_U]
 
-    def _head_params(self):
-        """The head's parameters in kernel order, cached per module structure (the per-bag caller of
-        infer.py:187-191 would otherwise walk nn.Module attribute lookups on every call)."""
-        mods = self._modules
-        skey = (self.shared_attention, id(mods.get("attention_V")), id(mods.get("attention_U")),
-                id(mods.get("attention_weights")), id(mods.get("classifiers")))
-        hit = self.__dict__.get("_head_param_cache")
-        if hit is not None and hit[0] == skey:
-            return hit[1]
+    def _head_slots(self):
+        """(module, parameter name) of every head parameter, in kernel order."""
         lv, lu = self._gate_linears()
-        params = [p for m in lv + lu for p in (m.weight, m.bias)]
-        params += [p for m in self.attention_weights for p in (m.weight, m.bias)]
-        params += [m.weight for m in self.classifiers]
-        self.__dict__["_head_param_cache"] = (skey, params)
+        slots = [(m, n) for m in lv + lu for n in ("weight", "bias")]
+        slots += [(m, n) for m in self.attention_weights for n in ("weight", "bias")]
+        slots += [(m, "weight") for m in self.classifiers]
+        return slots
+
+    def _head_params(self):
+        """The head's parameters in kernel order. The list is cached (the per-bag caller of
+        infer.py:187-191 would otherwise walk nn.Module attribute lookups on every call) and
+        revalidated on every call by identity, with plain dict lookups: every module on the path
+        from self to each parameter's owner, and the Parameter object in its owner's _parameters.
+        So replacing a Linear inside a container, assigning a new Parameter, or
+        load_state_dict(..., assign=True) all miss the cache; the cache holds the objects it
+        compares against, so an id cannot be reused while it is alive."""
+        hit = self.__dict__.get("_head_param_cache")
+        if hit is not None and self.shared_attention == hit[0]:
+            chains, slots, params = hit[1:]
+            try:
+                ok = all(_walk(self, path) is m for path, m in chains) and \
+                    all(m._parameters.get(n) is p for (m, n), p in zip(slots, params))
+            except KeyError:
+                ok = False
+            if ok:
+                return params
+        slots = self._head_slots()
+        params = [m._parameters[n] for m, n in slots]
+        names = {id(m): name for name, m in self.named_modules()}
+        owners = {id(m): m for m, _ in slots}
+        chains = [(tuple(names[i].split(".")), m) for i, m in owners.items()]
+        self.__dict__["_head_param_cache"] = (self.shared_attention, chains, slots, params)
         return params
 
     def head_tensors(self, device) -> ops.HeadTensors:

@@ -6,6 +6,7 @@ Reference semantics served: MultiHeadGatedAttentionMIL.mc_inference (reference m
 from the extracted features H on, for a whole batch of bags at once.
 """
 import ctypes
+import weakref
 from typing import NamedTuple, Optional, Sequence, Union
 
 import torch
@@ -61,13 +62,22 @@ def _require_cuda(name, t, dtype=None):
         raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
 
 
-_CHECKED_HEADS: dict = {}     # id -> (head, device): heads already validated (per-call host time)
+# heads already validated (per-call host time): id(head) -> (weak references to its tensors, the
+# device, each tensor's (data_ptr, stride)). No strong reference: a dropped model's GPU weights are
+# freed. A hit needs the same tensor objects at the same storage and layout, so rebinding a field
+# with `t.data = other` is validated again.
+_CHECKED_HEADS: dict = {}
+
+
+def _head_fingerprint(head: HeadTensors):
+    return tuple((t.data_ptr(), t.stride()) for t in head)
 
 
 def _check_head(head: HeadTensors, device):
     hit = _CHECKED_HEADS.get(id(head))
-    if hit is not None and hit[0] is head and hit[1] == device:
-        return                    # same tensors: dtype, layout and device cannot have changed
+    if hit is not None and hit[1] == device and all(r() is t for r, t in zip(hit[0], head)) and \
+            hit[2] == _head_fingerprint(head):
+        return                    # same tensors, storage and layout: dtype and device unchanged
     for name, t in zip(head._fields, head):
         _require_cuda(name, t, torch.float32)
         if not t.is_contiguous():
@@ -76,7 +86,7 @@ def _check_head(head: HeadTensors, device):
             raise ValueError(f"{name} is on {t.device}, H on {device}")
     if len(_CHECKED_HEADS) > 16:
         _CHECKED_HEADS.clear()
-    _CHECKED_HEADS[id(head)] = (head, device)
+    _CHECKED_HEADS[id(head)] = (tuple(weakref.ref(t) for t in head), device, _head_fingerprint(head))
 
 
 class BagOffsets(torch.Tensor):

@@ -52,7 +52,8 @@ def main():
     F = B * flops_per_bag(N, T, L, D, C, C)
 
     def launch(lib, fused):
-        os.environ["MCGMIL_FUSED"] = "1" if fused else "0"
+        # the path through args.flags: MCGMIL_FUSED is read once per process
+        a.flags = (a.flags & ~3) | (_lib.PATH_FLAGS["fused"] if fused else _lib.PATH_FLAGS["two_kernel"])
         if fused:
             _lib.check(lib.mcgmil_gate_softmax_pool(pa, sh), "gate_softmax_pool")
         else:

@@ -33,7 +33,7 @@ def test_gpus_flag_spawns_ranks(cuda):
     one-GPU rehearsal of the driver's multi-GPU run) and rank 0 reports n_gpus = 2."""
     r = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "2", "--same-device", "--dist-backend",
                         "gloo", "--steps", "2", "--warmup", "1", "--bags", "4", "--no-cpu-baseline",
-                        "--busy-seconds", "1"],
+                        "--busy-seconds", "1", "--no-calibration"],
                        env=_env(), capture_output=True, text=True, timeout=600, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -8,12 +8,13 @@ import pytest
 
 from conftest import REPO
 
-HEADERS = [os.path.join(REPO, "include", h) for h in ("mcgmil.h", "mcgmil_image.h", "mcgmil_features.h")]
+HEADERS = [os.path.join(REPO, "include", h) for h in ("mcgmil.h", "mcgmil_image.h", "mcgmil_features.h",
+                                                            "mcgmil_calib.h")]
 
 
 def declared_functions():
     src = "".join(open(h).read() for h in HEADERS)
-    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(mcgmil_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|size_t|const char\*)\s+(mcgmil_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_entry_points():
@@ -42,7 +43,7 @@ def test_library_targets_gfx950(hip_lib):
 
 def test_args_struct_matches_binding(hip_lib):
     from mcgmil import _lib
-    assert hip_lib.mcgmil_abi_version() == 4 == _lib.ABI_VERSION
+    assert hip_lib.mcgmil_abi_version() == 5 == _lib.ABI_VERSION
     assert hip_lib.mcgmil_conv_args_size() == ctypes.sizeof(_lib.ConvArgs)
     assert hip_lib.mcgmil_stem_args_size() == ctypes.sizeof(_lib.StemArgs)
     assert hip_lib.mcgmil_args_size() == ctypes.sizeof(_lib.Args)
@@ -72,9 +73,6 @@ def test_workspace_size_formula(hip_lib):
     rc, n = _ws(hip_lib, _args())
     assert rc == 0
     packed = (2 * 16 + 1) * 16 * 512 * 2                     # (2P+1) tiles x KS x 512 x bf16
-    # + the row-owner kernel's stream (mcgmil_rowgate.h): L/16 K steps x 2GD/32 blocks x 1 KiB,
-    # then the classifier table [4][L] bf16, after a 256-byte alignment
-    packed = ((packed + 255) // 256) * 256 + (512 // 16) * (2 * 2 * 128 // 32) * 1024 + 4 * 512 * 2
     scores = 100 * 2048 * 2 * 4
     plan = ((100 * 2048 // 16 * 4 + 255) // 256) * 256      # tile plan (int32 per 16-row tile)
     regions = 256                                            # fused region plan: int32 [B+1]
@@ -87,7 +85,7 @@ def test_workspace_size_formula(hip_lib):
     ("L", 500, -2), ("L", 4096, -2), ("D", 100, -2), ("C", 5, -2), ("C", 0, -2), ("G", 3, -1),
     ("T", 0, -1), ("num_bags", 0, -1), ("p_feat", 1.5, -1), ("p_att", -0.1, -1),
     ("h_dtype", 7, -1), ("bag_offsets", None, -1), ("total_rows", -1, -1),
-    ("flags", 3, -1), ("flags", 16, -1), ("flags", 32, -1), ("reserved", 1, -1),
+    ("flags", 3, -1), ("flags", 12, -1), ("flags", 16, -1), ("flags", 32, -1), ("reserved", 1, -1),
 ])
 def test_validation_errors(hip_lib, field, value, code):
     rc, _ = _ws(hip_lib, _args(**{field: value}))
@@ -110,7 +108,7 @@ def test_path_flags_select_the_launch(hip_lib, monkeypatch):
     """mcgmil_args.flags picks the launch mcgmil_gate_softmax_pool makes (host logic, no launch):
     auto = fused only for bf16 batches of equal-size bags with >= 16,384 regions; FUSED whenever
     it applies; TWO_KERNEL never; MCGMIL_GATE_PP keeps bf16 heads off the fused (pipe) tile code;
-    MCGMIL_GATE_ROW takes the row-gate fused launch."""
+    bf16 shared heads fuse only when forced (auto keeps gate_pp_kernel)."""
     from mcgmil import _lib
     F, G = _lib.PATH_FLAGS, _lib.GATE_FLAGS
     small = dict(num_bags=16, total_rows=16 * 2048, uniform_bag_rows=2048)
@@ -121,7 +119,9 @@ def test_path_flags_select_the_launch(hip_lib, monkeypatch):
     assert _regions(hip_lib, _args(flags=F["two_kernel"], **big)) == 0
     assert _regions(hip_lib, _args(flags=F["fused"] | G["pp"], **small)) == 0
     assert _regions(hip_lib, _args(flags=F["fused"] | G["pipe"], **small)) == 16 * 50
-    assert _regions(hip_lib, _args(flags=F["fused"] | G["row"], **small)) == 16 * 50
+    assert _regions(hip_lib, _args(G=1, **big)) == 0                          # shared: auto stays off
+    assert _regions(hip_lib, _args(G=1, flags=F["fused"], **small)) == 16 * 50
+    assert _regions(hip_lib, _args(G=1, flags=G["pipe"], **big)) == 512 * 50
     assert _regions(hip_lib, _args(flags=F["fused"], h_dtype=_lib.MCGMIL_F32, **small)) == 16 * 50
     assert _regions(hip_lib, _args(h_dtype=_lib.MCGMIL_F32, **big)) == 0      # fp32: auto stays off
 
@@ -173,6 +173,20 @@ def test_gate_rejects_misaligned_H(hip_lib):
     assert hip_lib.mcgmil_gate_scores(ctypes.byref(a), None) == -3
     a.H, a.ldh = ctypes.c_void_p(0x3000), 509
     assert hip_lib.mcgmil_gate_scores(ctypes.byref(a), None) == -1  # ldh < L
+
+
+def test_mfma_calib_sizes_and_validation(hip_lib):
+    """mcgmil_calib.h: FLOPs per workgroup-step (8 waves x 32 bf16 16x16x32 / 128 fp32 16x16x4
+    MFMAs) and the argument checks (no launches)."""
+    from mcgmil import _lib
+    assert hip_lib.mcgmil_mfma_calib_flops_per_step(_lib.MCGMIL_BF16) == 8 * 32 * 16 * 16 * 32 * 2
+    assert hip_lib.mcgmil_mfma_calib_flops_per_step(_lib.MCGMIL_F32) == 8 * 128 * 16 * 16 * 4 * 2
+    assert hip_lib.mcgmil_mfma_calib_flops_per_step(7) == 0
+    sink = ctypes.c_void_p(0x1000)
+    assert hip_lib.mcgmil_mfma_calib(7, 256, 10, 1, sink, None, None) == -1
+    assert hip_lib.mcgmil_mfma_calib(_lib.MCGMIL_BF16, 0, 10, 1, sink, None, None) == -1
+    assert hip_lib.mcgmil_mfma_calib(_lib.MCGMIL_BF16, 256, 0, 1, sink, None, None) == -1
+    assert hip_lib.mcgmil_mfma_calib(_lib.MCGMIL_BF16, 256, 10, 1, None, None, None) == -1
 
 
 def _bn(**kw):

@@ -11,10 +11,6 @@ mcgmil_fused.hip compiled with the library's own flags (mcgmil/_build.py; hipcc 
   conv3x3_halo_kernel; every
   STATS / input-BN instantiation) have no scratch and fit 256 registers: they run one 8-wave
   workgroup per CU (two waves per SIMD), and a spill would put scratch traffic into the tap loop;
-* every row-owner gate kernel (rowgate_scores_kernel, rowgate_fused_kernel; mcgmil_rowgate.h) has
-  no scratch: the LDS-DMA instantiations read the weight ring with inline-asm ds_reads whose
-  destination registers the compiler cannot see in flight, so a spill or copy of one of them before
-  its wait would read stale data (the register-staged instantiations are compiler-visible);
 * the stem convolution (stem_conv_kernel) drains its LDS-DMA staging (s_waitcnt vmcnt(0)) right
   before every barrier that publishes a staged tile: its epilogue's LDS accesses are inline asm the
   compiler's wait-count pass cannot see, so nothing else would order them after the DMA.
@@ -100,34 +96,6 @@ def test_fused_kernel_fits_without_spills(fused_asm):
     for sym in (FUSED, FUSED_PROBE):
         assert kernel_meta(fused_asm, sym, "private_seg_size") == 0, sym
         assert kernel_meta(fused_asm, sym, "num_vgpr") + kernel_meta(fused_asm, sym, "num_agpr") <= 256, sym
-
-
-def test_pp_fused_kernel_fits(fused_asm):
-    # gate_pp_fused_kernel (opt-in single launch for shared heads): two workgroups per CU, so <= 256
-    # registers; the Philox instantiations keep one 8-byte value in scratch, stored before the tile
-    # loop and reloaded once per 128-row tile outside the K loop (12 bytes of frame) -- more would mean
-    # spills in the tile code itself
-    syms = set(re.findall(r"\.set (_ZN6mcgmil20gate_pp_fused_kernel\w*)\.private_seg_size", fused_asm))
-    assert len(syms) == 8, syms       # MAXC in {2, 4} x one class per wave or not x clock probe
-    for sym in syms:
-        assert kernel_meta(fused_asm, sym, "private_seg_size") <= 16, sym
-        assert kernel_meta(fused_asm, sym, "num_vgpr") + kernel_meta(fused_asm, sym, "num_agpr") <= 256, sym
-
-
-def _rowgate_syms(text, kind):
-    return set(re.findall(rf"\.set (_ZN6mcgmil\d+rowgate_{kind}_kernel\w*)\.private_seg_size", text))
-
-
-def test_rowgate_kernels_fit_without_spills(device_asm, fused_asm):
-    scores, fused = _rowgate_syms(device_asm, "scores"), _rowgate_syms(fused_asm, "fused")
-    # G in {1, 2} x MAXC in {2, 4} x {Philox, replayed masks}; the fused kernel makes its own masks
-    assert len(scores) == 8 and len(fused) == 4, (scores, fused)
-    assert any(s.endswith("Lb1EEEvNS_10GateParamsE") for s in scores | fused), "no LDS-DMA instantiation"
-    for text, syms in ((device_asm, scores), (fused_asm, fused)):
-        for sym in syms:
-            assert kernel_meta(text, sym, "private_seg_size") == 0, sym
-            # one wave per SIMD: the whole unified register file
-            assert kernel_meta(text, sym, "num_vgpr") + kernel_meta(text, sym, "num_agpr") <= 512, sym
 
 
 @pytest.fixture(scope="module")

@@ -1,5 +1,5 @@
-"""The single-launch hot path (gate_fused_kernel, or gate_pp_fused_kernel for bf16 heads of <= 8
-gate tile pairs, via mcgmil_gate_softmax_pool, reference model.py:280-316) against the two-kernel
+"""The single-launch hot path (gate_fused_kernel via mcgmil_gate_softmax_pool, reference
+model.py:280-316) against the two-kernel
 path (gate_pipe_kernel / gate_pp_kernel -> workspace -> softmax_pool_kernel) and against the
 reference's golden outputs.
 
@@ -51,8 +51,8 @@ CASES = [
     ("f32_shared_uniform_N96", torch.float32, [96] * 5, 40, 2, True, 128),
     ("f32_c4_sep_ragged", torch.float32, [50, 1500, 1024, 1025, 3], 4, 4, False, 64),
     ("bf16_c1_ragged", torch.bfloat16, [33, 4000, 5], 9, 1, False, 128),
-    # bf16 heads of <= 8 gate tile pairs: gate_pp_fused_kernel (regions of <= 2048 rows, C <= 2;
-    # 512 for C = 4), incl. bags over the cap and the one-class-per-wave tile (D = 64 separate heads)
+    # bf16 heads of <= 8 gate tile pairs (two-kernel path: gate_pp_kernel; forced fused: the 8-wave
+    # tile with one pair per wave), incl. bags over the cap and D = 64 separate heads
     ("bf16_shared_uniform_N2048", torch.bfloat16, [2048] * 3, 7, 2, True, 128),
     ("bf16_shared_uniform_N300", torch.bfloat16, [300] * 4, 30, 2, True, 128),
     ("bf16_shared_ragged", torch.bfloat16, [300, 0, 5000, 1, 129, 2048, 2049, 777], 5, 2, True, 128),
@@ -111,12 +111,13 @@ def test_fused_auto_policy(cuda):
     offs32 = ops.bag_offsets_tensor([512] * 1280, cuda)
     assert regions(big32, offs32, head, 100) == 0
     assert regions(big32, offs32, head, 100, path="fused") == 1280 * 13
-    # bf16 shared heads (gate_pp_fused_kernel) stay on the two-kernel path under auto (0.7% slower
-    # fused, profiles/r05/pp_fused_probe.log); forced: one t-group of 2048 rows per region
+    # bf16 shared heads stay on gate_pp_kernel + softmax_pool_kernel under auto (the fused 8-wave
+    # tile measured 5.53 vs 4.04-4.10 ms per 64 bags); forced: the 8-wave tile, two t-groups per region
     sd = synthetic.head_state_dict(0, C=2, shared=True)
     shead = head_on(synthetic.head_arrays(sd, 2, True), cuda)
     assert regions(big, big_offs, shead, 100) == 0
-    assert regions(big, big_offs, shead, 100, path="fused") == 512 * 100
+    assert regions(big, big_offs, shead, 100, path="fused") == 512 * 50
+    assert regions(big, big_offs, shead, 100, path="fused", gate="pp") == 0
 
 
 from test_gpu_parity import BF16_CASES, FP32_CASES, TOL32, TOL_BF16_IN, compare, run  # noqa: E402
@@ -125,7 +126,7 @@ from test_gpu_parity import BF16_CASES, FP32_CASES, TOL32, TOL_BF16_IN, compare,
 @pytest.mark.parametrize("name", FP32_CASES + BF16_CASES)
 def test_fused_matches_reference_goldens(cuda, name):
     """The fused launch (forced) on every reference-made golden MC case, with the kernel's own
-    Philox masks, at the bounds of tests/test_gpu_parity.py (bf16 shared heads: gate_pp_fused_kernel)."""
+    Philox masks, at the bounds of tests/test_gpu_parity.py."""
     case = Case(name)
     bf16 = name in BF16_CASES
     out = run(case, cuda, torch.bfloat16 if bf16 else torch.float32, path="fused")
@@ -266,76 +267,6 @@ def test_path_and_gate_flags_agree(cuda):
         assert torch.equal(a[k], b[k]) and torch.equal(a[k], c[k]), k
     with pytest.raises(ValueError):
         ops.mcdo_forward(H, offs, head, 30, path="bogus", **kw)
-
-
-# ------------------------------------------------------------------ the row-owner gate kernel
-ROW_CASES = [
-    # name, sizes, T, C, shared, p_feat, p_att
-    ("sep_uniform", [2048] * 2, 6, 2, False, 0.1, 0.1),
-    ("shared_uniform", [2048] * 2, 6, 2, True, 0.1, 0.1),
-    ("sep_ragged", [1, 37, 200, 513, 0, 130, 4100], 5, 2, False, 0.1, 0.5),
-    ("shared_ragged_c3", [129, 3, 640, 5000], 7, 3, True, 0.37, 0.1),
-    ("sep_c4", [300, 77], 4, 4, False, 0.1, 0.1),
-    ("sep_c1_p0", [300], 3, 1, False, 0.0, 0.0),
-    ("sep_p1", [100, 64], 2, 2, False, 1.0, 1.0),
-]
-
-
-@pytest.mark.parametrize("case", ROW_CASES, ids=[c[0] for c in ROW_CASES])
-def test_row_gate_fused_two_kernel_oracle(cuda, case):
-    """gate="row" (MCGMIL_GATE_ROW: rowgate_scores_kernel / rowgate_fused_kernel, mcgmil_rowgate.h):
-    fused and two-kernel launches bitwise equal, and every non-empty bag against the reference
-    restatement (mcdo_ref, model.py:280-316) with the kernel's own masks on the same bf16 operands."""
-    from mcgmil import ops
-    from test_gpu_parity import TOL_BF16_IN
-    name, sizes, T, C, shared, p_f, p_a = case
-    L, seed = 512, 808
-    sd = synthetic.head_state_dict(seed, L=L, C=C, shared=shared)
-    Hs = [synthetic.bf16_round(synthetic.bag_features(seed + 10 + b, n, L)) for b, n in enumerate(sizes)]
-    head = head_on(synthetic.head_arrays(sd, C, shared), cuda)
-    H = torch.from_numpy(np.concatenate(Hs)).to(cuda).bfloat16().contiguous()
-    offs = ops.bag_offsets_tensor(sizes, cuda)
-    kw = dict(p_feat=p_f, p_att=p_a, seed=seed, bag_id_base=3, return_stats=True, gate="row")
-    # the row kernel runs one or two gates; four separate heads fall back to the tile kernels
-    assert (regions(H, offs, head, T, path="fused", gate="row") > 0) == (head.G <= 2)
-    two = ops.mcdo_forward(H, offs, head, T, path="two_kernel", **kw)
-    fz = ops.mcdo_forward(H, offs, head, T, path="fused", **kw)
-    torch.cuda.synchronize()
-    for k in two:
-        assert torch.equal(torch.nan_to_num(fz[k], nan=7.0), torch.nan_to_num(two[k], nan=7.0)), k
-    prm = mcdo_ref.HeadParams(synthetic.head_arrays(synthetic.round_state_dict_bf16(sd), C, shared))
-    Y = two["Y"].cpu().numpy()
-    A = ops.split_bags(two["A"].cpu(), sizes, T * C)
-    for b, n in enumerate(sizes):
-        if n == 0:
-            assert np.all(Y[b] == 0)
-            continue
-        kF, kA = mcdo_ref.masks_for_bag(seed, 3 + b, T, n, L, C, p_f, p_a)
-        Yr, Ar = mcdo_ref.mc_inference(Hs[b], prm, kF, kA, p_f, p_a)
-        np.testing.assert_allclose(Y[b], Yr[:, 0].numpy(), rtol=0, atol=TOL_BF16_IN["Y"])
-        Ar = Ar[:, 0].numpy()
-        assert np.abs(A[b].numpy().reshape(T, C, n) - Ar).max() <= TOL_BF16_IN["A"] * max(np.abs(Ar).max(), 1e-30)
-
-
-@pytest.mark.parametrize("shared", [False, True])
-def test_row_gate_replayed_masks_equal_philox(cuda, shared):
-    """The row kernel with the masks handed in (keep_feat / keep_att, the replay instantiations:
-    register-staged weights for C = 4 separate heads, LDS-DMA otherwise) is bitwise its own Philox run."""
-    from mcgmil import ops
-    for C in (2, 4):
-        sizes, T = [700, 33], 4
-        sd = synthetic.head_state_dict(3, L=512, C=C, shared=shared)
-        head = head_on(synthetic.head_arrays(sd, C, shared), cuda)
-        H = torch.from_numpy(np.concatenate([synthetic.bag_features(9 + b, n, 512) for b, n in enumerate(sizes)])) \
-            .to(cuda).bfloat16().contiguous()
-        offs = ops.bag_offsets_tensor(sizes, cuda)
-        R = sum(sizes)
-        kf = ops.feature_keep(offs, R, T, 512, 0.1, 11)
-        ka = ops.attention_keep(offs, R, T, C, 0.1, 11)
-        kw = dict(p_feat=0.1, p_att=0.1, seed=11, path="two_kernel", gate="row")
-        a = ops.mcdo_forward(H, offs, head, T, **kw)
-        b = ops.mcdo_forward(H, offs, head, T, keep_feat=kf, keep_att=ka, **kw)
-        assert torch.equal(a["Y"], b["Y"]) and torch.equal(a["A"], b["A"]), C
 
 
 def _random_cases(n=12, seed=2024):

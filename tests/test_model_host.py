@@ -130,3 +130,32 @@ def test_reference_checkpoint_loads_strictly(tmp_path, cfg):
     own = m.state_dict()
     for k, v in sd.items():
         assert torch.equal(own[k], v), k
+
+
+@pytest.mark.parametrize("shared", [True, False])
+def test_head_param_cache_sees_replaced_modules_and_parameters(shared):
+    """_head_params (the per-bag caller's cached parameter list, model.py:182-203 order) follows a
+    replaced Linear inside a container, a newly assigned Parameter and load_state_dict(assign=True);
+    an unchanged module keeps the cached list."""
+    import torch.nn as nn
+    from mcgmil import MultiHeadGatedAttentionMIL
+    m = MultiHeadGatedAttentionMIL(pretrained=False, shared_attention=shared)
+    p0 = m._head_params()
+    assert m._head_params() is p0                                    # hit: same list object
+    new_w = nn.Parameter(torch.randn_like(m.classifiers[0].weight))
+    m.classifiers[0].weight = new_w
+    p1 = m._head_params()
+    assert p1 is not p0 and any(p is new_w for p in p1)
+    lin = nn.Linear(m.L, m.D)
+    if shared:
+        m.attention_V[0] = lin
+    else:
+        m.attention_V[1][0] = lin
+    p2 = m._head_params()
+    assert any(p is lin.weight for p in p2) and any(p is lin.bias for p in p2)
+    sd = {k: v.clone() + 1 for k, v in m.state_dict().items() if not k.startswith("feature_extractor")}
+    m.load_state_dict(sd, strict=False, assign=True)
+    p3 = m._head_params()
+    assert all(m2._parameters[n] is p for (m2, n), p in zip(m._head_slots(), p3))
+    assert not any(p is q for p in p3 for q in p2)                   # every parameter was replaced
+    assert len(p3) == len(p0)
