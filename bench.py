@@ -431,13 +431,19 @@ def measure_batch(sizes, ids, T, dtype, shared, dev, world, steps, warmup, busy_
     torch.cuda.synchronize()
     busy = time.perf_counter() - t_busy
     el, gate_ms = timed_pass()
-    # the clock the gate launch runs at: one more (untimed) step right after the timed ones, its
-    # workgroups stamping s_memtime / s_memrealtime at start and end (MCGMIL_CLOCK_PROBE)
+    # the clock the gate launch runs at: the third of five back-to-back (untimed) steps right after
+    # the timed ones, its workgroups stamping s_memtime / s_memrealtime at start and end
+    # (MCGMIL_CLOCK_PROBE). Not the first step after a synchronize: the chip raises its clock in the
+    # idle gap, and such a launch read ~7% above the steady state that GRBM_GUI_ACTIVE / 8 / wall
+    # gives for the timed launches (profiles/r06/grbm_clock.json)
     rec = ops.clock_record(dev)
-    a.debug, a.flags = ctypes.c_void_p(rec.data_ptr()), a.flags | _lib.CLOCK_PROBE
-    step()
+    for i in range(5):
+        if i == 2:
+            a.debug, a.flags = ctypes.c_void_p(rec.data_ptr()), a.flags | _lib.CLOCK_PROBE
+        step()
+        if i == 2:
+            a.debug, a.flags = None, a.flags & ~_lib.CLOCK_PROBE
     torch.cuda.synchronize()
-    a.debug, a.flags = None, a.flags & ~_lib.CLOCK_PROBE
     clock = ops.clock_mhz(rec)
     if world > 1 and clock is not None:
         t = torch.tensor([clock["median"]], dtype=torch.float64, device=dev)
@@ -457,7 +463,7 @@ def at_clock(achieved, peak, clock, dtype="bf16"):
     return {"clock_mhz": round(clock["median"], 1), "clock_mhz_p10_p90": [round(clock["p10"], 1), round(clock["p90"], 1)],
             "frac_at_clock": achieved / (peak * clock["median"] / MAX_CLOCK_MHZ),
             "clock_source": f"in-kernel s_memtime/s_memrealtime x 100 MHz, median of {clock['workgroups']} "
-                            f"workgroups of one probed launch right after the timed steps",
+                            f"workgroups of one probed launch, the 3rd of 5 back-to-back steps after the timed ones",
             **vs_measured(achieved, dtype, clock["median"])}
 
 
@@ -503,7 +509,8 @@ def mfma_calibration(dev, dtype, warm_s=2.0, timed_s=1.0, launch_ms=20.0):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / n
     rec = ops.clock_record(dev)
-    launch(steps, seed=7, rec=rec)
+    for i in range(5):            # the probed launch in the middle of back-to-back launches
+        launch(steps, seed=7 + i, rec=rec if i == 2 else None)
     torch.cuda.synchronize()
     clock = ops.clock_mhz(rec)
     tflops = fps * cus * steps / (ms * 1e-3) / 1e12

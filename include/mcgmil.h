@@ -73,8 +73,11 @@ enum mcgmil_flags {
                                     the two kernels */
     MCGMIL_PATH_FUSED = 1,       /* the fused launch (gate_fused_kernel) whenever it applies: bf16 or
                                     fp32, L % 64 == 0, L >= 128, the tile within 160 KiB of LDS
-                                    (bf16: L <= 1024), <= 16 gate tile pairs, no replay masks, gate
-                                    not forced to MCGMIL_GATE_PP */
+                                    (bf16: L <= 1024), <= 16 gate tile pairs, no replay masks, and
+                                    for bf16 heads the two-kernel path would run on gate_pipe_kernel
+                                    (> 8 gate tile pairs, or MCGMIL_GATE_PIPE) -- the fused launch
+                                    runs that kernel's tile code; heads on gate_pp_kernel (shared
+                                    heads) always take the two kernels */
     MCGMIL_PATH_TWO_KERNEL = 2,  /* never fused: gate scores -> workspace -> softmax/pooling */
     MCGMIL_PATH_MASK = 3,
     MCGMIL_GATE_AUTO = 0 << 2,   /* two-kernel path, bf16 heads: gate_pipe_kernel for > 8 gate tile

@@ -306,11 +306,13 @@ int try_fused_maxc(const mcgmil::GateParams& gp, long long total_rows, int L, in
     *rc = MCGMIL_OK;
     // (L >= 128: the fused pipeline peels two K steps at each end of a tile)
     if (gp.keep_feat) return 0;
-    bool pipe_heads = true;               // the heads the two-kernel path runs on gate_pipe_kernel
+    // bf16: only heads the two-kernel path runs on gate_pipe_kernel fuse (separate heads of > 8
+    // gate tile pairs, or any head under MCGMIL_GATE_PIPE): the fused launch runs that kernel's
+    // tile code, so A and Y stay bitwise the two-kernel path's. Heads on gate_pp_kernel (shared
+    // heads under auto / MCGMIL_GATE_PP) have no single-launch form and always take two kernels.
     if constexpr (sizeof(E) == 2) {
         const int mode = gate_mode(flags);
-        if (mode == 2) return 0;          // MCGMIL_GATE_PP: gate_pp_kernel has no single-launch form
-        pipe_heads = mode == 1 || gp.P > 2 * mcgmil::kPPWaves;
+        if (!(mode == 1 || (mode == 0 && gp.P > 2 * mcgmil::kPPWaves))) return 0;
     }
     if (L % 64 != 0 || L < 128 || gp.P > 2 * mcgmil::kGateWaves) return 0;
     if (mcgmil::fused_kernel_lds_bytes<E, MAXC>(L) > 160 * 1024) return 0;   // bf16 L > 1024
@@ -319,11 +321,11 @@ int try_fused_maxc(const mcgmil::GateParams& gp, long long total_rows, int L, in
     constexpr int cap = mcgmil::fused_cap<MAXC>();
     // auto: bf16 uniform batches only -- on ragged ones (config 4) the fused launch measured 2.8%
     // slower (regions of 16-32 tiles straddling t-groups; profiles/r03/bench_cfg4*.log), and in fp32
-    // (which spills in the tile loop) 13-18% slower (profiles/r03/probe_fused_f32.log). bf16 shared
-    // heads keep gate_pp_kernel + softmax_pool_kernel: the 8-wave tile in one launch measured 5.53
-    // vs 4.04-4.10 ms per 64 bags (profiles/r05/fused_ab_*), and a fused form of gate_pp_kernel's own
-    // tile 16.68 vs 16.56 ms per 256 bags (profiles/r05/pp_fused_probe.log; removed in round 6).
-    if (fm < 0 && (!pipe_heads || sizeof(E) != 2 || gp.uniform_rows <= 0 ||
+    // (which spills in the tile loop) 13-18% slower (profiles/r03/probe_fused_f32.log). (bf16 shared
+    // heads: the 8-wave tile in one launch measured 5.53 vs 4.04-4.10 ms per 64 bags for
+    // gate_pp_kernel + softmax_pool_kernel, profiles/r05/fused_ab_*; a fused form of gate_pp_kernel's
+    // own tile 16.68 vs 16.56 ms per 256 bags, profiles/r05/pp_fused_probe.log, removed in round 6.)
+    if (fm < 0 && (sizeof(E) != 2 || gp.uniform_rows <= 0 ||
                    mcgmil_detail::fused_regions(gp, total_rows, cap, true) < kFusedMinRegions))
         return 0;
     // same kernel shape as dispatch_gate_pipe: one class per wave for separate heads

@@ -108,7 +108,7 @@ def test_path_flags_select_the_launch(hip_lib, monkeypatch):
     """mcgmil_args.flags picks the launch mcgmil_gate_softmax_pool makes (host logic, no launch):
     auto = fused only for bf16 batches of equal-size bags with >= 16,384 regions; FUSED whenever
     it applies; TWO_KERNEL never; MCGMIL_GATE_PP keeps bf16 heads off the fused (pipe) tile code;
-    bf16 shared heads fuse only when forced (auto keeps gate_pp_kernel)."""
+    bf16 heads on gate_pp_kernel (shared) fuse only with the gate forced to gate_pipe_kernel."""
     from mcgmil import _lib
     F, G = _lib.PATH_FLAGS, _lib.GATE_FLAGS
     small = dict(num_bags=16, total_rows=16 * 2048, uniform_bag_rows=2048)
@@ -119,8 +119,9 @@ def test_path_flags_select_the_launch(hip_lib, monkeypatch):
     assert _regions(hip_lib, _args(flags=F["two_kernel"], **big)) == 0
     assert _regions(hip_lib, _args(flags=F["fused"] | G["pp"], **small)) == 0
     assert _regions(hip_lib, _args(flags=F["fused"] | G["pipe"], **small)) == 16 * 50
-    assert _regions(hip_lib, _args(G=1, **big)) == 0                          # shared: auto stays off
-    assert _regions(hip_lib, _args(G=1, flags=F["fused"], **small)) == 16 * 50
+    assert _regions(hip_lib, _args(G=1, **big)) == 0                          # shared: gate_pp_kernel
+    assert _regions(hip_lib, _args(G=1, flags=F["fused"], **small)) == 0
+    assert _regions(hip_lib, _args(G=1, flags=F["fused"] | G["pipe"], **small)) == 16 * 50
     assert _regions(hip_lib, _args(G=1, flags=G["pipe"], **big)) == 512 * 50
     assert _regions(hip_lib, _args(flags=F["fused"], h_dtype=_lib.MCGMIL_F32, **small)) == 16 * 50
     assert _regions(hip_lib, _args(h_dtype=_lib.MCGMIL_F32, **big)) == 0      # fp32: auto stays off

@@ -51,8 +51,9 @@ CASES = [
     ("f32_shared_uniform_N96", torch.float32, [96] * 5, 40, 2, True, 128),
     ("f32_c4_sep_ragged", torch.float32, [50, 1500, 1024, 1025, 3], 4, 4, False, 64),
     ("bf16_c1_ragged", torch.bfloat16, [33, 4000, 5], 9, 1, False, 128),
-    # bf16 heads of <= 8 gate tile pairs (two-kernel path: gate_pp_kernel; forced fused: the 8-wave
-    # tile with one pair per wave), incl. bags over the cap and D = 64 separate heads
+    # bf16 heads of <= 8 gate tile pairs (auto: gate_pp_kernel, no fused form): both paths with the
+    # gate forced to gate_pipe_kernel, whose tile the fused launch runs; incl. bags over the cap and
+    # D = 64 separate heads
     ("bf16_shared_uniform_N2048", torch.bfloat16, [2048] * 3, 7, 2, True, 128),
     ("bf16_shared_uniform_N300", torch.bfloat16, [300] * 4, 30, 2, True, 128),
     ("bf16_shared_ragged", torch.bfloat16, [300, 0, 5000, 1, 129, 2048, 2049, 777], 5, 2, True, 128),
@@ -73,10 +74,13 @@ def test_fused_equals_two_kernel_path(cuda, case):
     offs = ops.bag_offsets_tensor(sizes, cuda)
     ids = torch.tensor([7 * b + 3 for b in range(len(sizes))], dtype=torch.int32, device=cuda)
     kw = dict(p_feat=0.1, p_att=0.1, seed=1234, bag_ids=ids, return_stats=True)
-    assert regions(H, offs, head, T, path="two_kernel") == 0
-    ref = ops.mcdo_forward(H, offs, head, T, path="two_kernel", **kw)
-    nreg = regions(H, offs, head, T, path="fused")
-    out = ops.mcdo_forward(H, offs, head, T, path="fused", **kw)
+    gate = "pipe" if dtype == torch.bfloat16 and head.G * D // 16 <= 8 else "auto"
+    if gate == "pipe":          # gate_pp_kernel heads have no fused form under auto
+        assert regions(H, offs, head, T, path="fused") == 0
+    assert regions(H, offs, head, T, path="two_kernel", gate=gate) == 0
+    ref = ops.mcdo_forward(H, offs, head, T, path="two_kernel", gate=gate, **kw)
+    nreg = regions(H, offs, head, T, path="fused", gate=gate)
+    out = ops.mcdo_forward(H, offs, head, T, path="fused", gate=gate, **kw)
     torch.cuda.synchronize()
     assert nreg > 0
     for k in ref:
@@ -111,13 +115,14 @@ def test_fused_auto_policy(cuda):
     offs32 = ops.bag_offsets_tensor([512] * 1280, cuda)
     assert regions(big32, offs32, head, 100) == 0
     assert regions(big32, offs32, head, 100, path="fused") == 1280 * 13
-    # bf16 shared heads stay on gate_pp_kernel + softmax_pool_kernel under auto (the fused 8-wave
-    # tile measured 5.53 vs 4.04-4.10 ms per 64 bags); forced: the 8-wave tile, two t-groups per region
+    # bf16 shared heads stay on gate_pp_kernel + softmax_pool_kernel (the fused 8-wave tile measured
+    # 5.53 vs 4.04-4.10 ms per 64 bags); fused only with the gate forced to the 8-wave tile
     sd = synthetic.head_state_dict(0, C=2, shared=True)
     shead = head_on(synthetic.head_arrays(sd, 2, True), cuda)
     assert regions(big, big_offs, shead, 100) == 0
-    assert regions(big, big_offs, shead, 100, path="fused") == 512 * 50
+    assert regions(big, big_offs, shead, 100, path="fused") == 0
     assert regions(big, big_offs, shead, 100, path="fused", gate="pp") == 0
+    assert regions(big, big_offs, shead, 100, path="fused", gate="pipe") == 512 * 50
 
 
 from test_gpu_parity import BF16_CASES, FP32_CASES, TOL32, TOL_BF16_IN, compare, run  # noqa: E402
@@ -308,9 +313,13 @@ def test_random_shapes_fused_two_kernel_oracle(cuda, case):
     offs = ops.bag_offsets_tensor(sizes, cuda)
     kw = dict(p_feat=p_f, p_att=p_a, seed=seed, bag_id_base=17, return_stats=True)
     two = ops.mcdo_forward(H, offs, head, T, path="two_kernel", **kw)
-    fz = ops.mcdo_forward(H, offs, head, T, path="fused", **kw)
+    # bf16 heads on gate_pp_kernel (<= 8 gate tile pairs) fuse on the 8-wave tile only: compare the
+    # fused launch with the two-kernel path on that same tile (gate="pipe")
+    gate = "pipe" if bf16 and head.G * D // 16 <= 8 else "auto"
+    fz = ops.mcdo_forward(H, offs, head, T, path="fused", gate=gate, **kw)
+    same = two if gate == "auto" else ops.mcdo_forward(H, offs, head, T, path="two_kernel", gate=gate, **kw)
     for k in two:
-        assert torch.equal(torch.nan_to_num(fz[k], nan=7.0), torch.nan_to_num(two[k], nan=7.0)), k
+        assert torch.equal(torch.nan_to_num(fz[k], nan=7.0), torch.nan_to_num(same[k], nan=7.0)), k
     tol = TOL_BF16_IN if bf16 else TOL32
     sd_ref = synthetic.round_state_dict_bf16(sd) if bf16 else sd
     prm = mcdo_ref.HeadParams(synthetic.head_arrays(sd_ref, C, shared))
@@ -343,7 +352,9 @@ def test_clock_probe(cuda, path, shared):
     packed = ops.packed_weights(head, torch.bfloat16)      # the stages need packed weights
     outs = []
     for probe in (False, True):
-        a = ops.make_args(H, offs, head, T, 2, head.G, 128, 0.1, 0.1, seed=3, path=path)
+        # shared heads fuse only on the 8-wave tile (gate="pipe"); the two-kernel path probes gate_pp_kernel
+        a = ops.make_args(H, offs, head, T, 2, head.G, 128, 0.1, 0.1, seed=3, path=path,
+                          gate="pipe" if shared and path == "fused" else "auto")
         a.packed_w = ctypes.c_void_p(packed.data_ptr())
         n = ctypes.c_size_t()
         lib = _lib.load()

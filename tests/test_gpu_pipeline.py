@@ -7,6 +7,8 @@ small size): every stage checked against its CPU counterpart on the same inputs.
   head       the GPU's own features through the MCDO oracle with the kernel's Philox masks:
              the fp32 bounds of tests/test_gpu_parity.py
   maps       mean/std of the oracle's attention maps from the kernel's A: abs <= 2.4e-7"""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -119,13 +121,42 @@ def test_mc_predict_image_bf16_features(cuda):
 # BASELINE config 5 itself (bench.py --workload cfg5: the 7036 x 2800 synthetic mammogram, 224-px
 # tiles at overlap 0.75 / empty_thresh 0.75, k = 1,507 instances, T = 100, the bench's model and
 # seed): the bf16 pipeline's uncertainty outputs against the fp32 pipeline's, whose features are
-# first checked against the same ResNet on the CPU. Measured in round 2
-# (profiles/r02/bench_cfg5_bf16.log) and again in round 3 (profiles/r03/probe_cfg5_drift.log):
-# A_mean nrel 9.9e-3, A_var nrel 4.1e-2, prob_mean 3.2e-5, Y 7.2e-4, features nrel 2.8e-2. The
-# bounds are 1.5x those. The drift enters in the backbone (the bf16 ResNet moves the features by
-# ~3% before the head; the bf16 head alone adds ~5e-3 to A_mean,
-# tests/test_gpu_parity.py::test_bf16_drift_vs_fp32_reference).
-CFG5_DRIFT = dict(A_mean=1.5 * 9.9e-3, A_var=1.5 * 4.1e-2, prob_mean=1.5 * 3.2e-5, Y=1.5 * 7.2e-4)
+# first checked against the same ResNet on the CPU.
+#
+# The bound is argued, not calibrated (verdict r05 item 5). The drift is the bf16 arithmetic of a
+# 17-convolution network, not this build's kernels: the same bf16 instances through PyTorch-ROCm's
+# own layers under torch.autocast (MIOpen bf16 convolutions, torch BN; MCGMIL_NATIVE_* = 0) drift
+# from the fp32 pipeline by the same amount. So each output of this build's bf16 pipeline must be
+# within 1.25x (+ an absolute floor) of the torch-autocast pipeline's drift on the same image,
+# seed and head -- the bound test_gpu_features.py applies to the backbone alone. A split-bf16
+# (hi + lo) variant of the weights, priced in round 6 (scripts/probe_split_bf16_drift.py,
+# profiles/r06/split_bf16_drift.log), cuts the emulated A_var drift by 15-25% at most, because
+# the stored bf16 activations carry the rest; DESIGN.md §7 has the table. Measured drift (rounds
+# 2-5): A_mean nrel 9.9e-3 - 1.0e-2, A_var nrel 4.1e-2 - 4.3e-2, features 2.7e-2 - 2.8e-2. The
+# fixed caps below are sanity limits only (2x the measured values).
+CFG5_REL_TO_TORCH = 1.25
+CFG5_FLOOR = dict(A_mean=1e-3, A_var=4e-3, prob_mean=1e-5, Y=1e-4, features=1e-3)
+CFG5_CAP = dict(A_mean=2e-2, A_var=8.5e-2, prob_mean=1e-4, Y=2e-3, features=6e-2)
+
+
+def _torch_autocast_pipeline(model, patcher, img, seed):
+    """The same bag through PyTorch-ROCm's own layers under torch.autocast (bf16 instances and
+    convolutions, torch BN) and this build's bf16 head: the drift an implementation-independent
+    bf16 pipeline shows. The MCGMIL_NATIVE_* switches are read per call (mcgmil/features.py)."""
+    from mcgmil.infer import mc_predict_image
+    keys = ("MCGMIL_FUSED_BN", "MCGMIL_NATIVE_CONV", "MCGMIL_NATIVE_STEM")
+    old = {k: os.environ.get(k) for k in keys}
+    try:
+        for k in keys:
+            os.environ[k] = "0"
+        model.compute_dtype = torch.bfloat16
+        return mc_predict_image(model, patcher, img, T=100, seed=seed, features_dtype=torch.bfloat16)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def test_cfg5_bf16_uncertainty_drift(cuda):
@@ -164,13 +195,18 @@ def test_cfg5_bf16_uncertainty_drift(cuda):
         f_cpu = cpu_model.extract_features(inst.cpu()[None])[0]
     assert nrel(a["features"].cpu().numpy(), f_cpu.numpy()) <= 1e-4
 
-    def nr(k):
-        x, y = b[k].double(), a[k].double()
-        return float((x - y).abs().max() / y.abs().max())
+    def drift(o):
+        def nr(k):
+            x, y = o[k].double(), a[k].double()
+            return float((x - y).abs().max() / y.abs().max())
+        return dict(A_mean=nr("A_mean"), A_var=nr("A_var"),
+                    prob_mean=float((a["prob_mean"] - o["prob_mean"]).abs().max()),
+                    Y=float((a["Y"] - o["Y"]).abs().max()), features=nr("features"))
 
-    d = dict(A_mean=nr("A_mean"), A_var=nr("A_var"),
-             prob_mean=float((a["prob_mean"] - b["prob_mean"]).abs().max()),
-             Y=float((a["Y"] - b["Y"]).abs().max()), features=nr("features"))
-    print("config-5 bf16-vs-fp32 drift: " + ", ".join(f"{k} {v:.3g}" for k, v in d.items()))
-    for k, bound in CFG5_DRIFT.items():
-        assert d[k] <= bound, (k, d[k], bound)
+    d = drift(b)
+    t = drift(_torch_autocast_pipeline(model, patcher, img, seed))
+    print("config-5 bf16-vs-fp32 drift: " + ", ".join(f"{k} {v:.3g} (torch autocast {t[k]:.3g})"
+                                                      for k, v in d.items()))
+    for k in CFG5_FLOOR:
+        assert d[k] <= CFG5_REL_TO_TORCH * t[k] + CFG5_FLOOR[k], (k, d[k], t[k])
+        assert d[k] <= CFG5_CAP[k], (k, d[k], CFG5_CAP[k])
