@@ -48,10 +48,11 @@ def bytes_per_bag(N, T, L, C, esize):
 
 def measured_traffic(N, T, B, dtype, shared, path_kind):
     """HBM bytes per gate launch from the committed rocprofv3 PMC passes (profiles/*/
-    gate_traffic.json, newest round first) when they were taken on this exact workload and
-    launch path ("fused": gate_fused_kernel; "pipe": gate_pipe_kernel)."""
+    gate_traffic*.json, newest round first) when they were taken on this exact workload and
+    launch path ("fused": gate_fused_kernel; "pipe": gate_pipe_kernel). N is "U(256,2048)" for
+    config 4's ragged batch."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "gate_traffic.json")),
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "gate_traffic*.json")),
                        reverse=True):
         t = json.load(open(path))
         if t.get("config") == {"bags": B, "N": N, "T": T, "dtype": dtype, "shared": shared} and \
@@ -249,8 +250,8 @@ def main():
     achieved = F / (gate_ms * 1e-3) / 1e12
     hbm_bytes = sum(bytes_per_bag(n, T, L, C, esize) for n in sizes) + nbytes_packed
     hbm_gbs = hbm_bytes / (gate_ms * 1e-3) / 1e9
-    traffic, traffic_src = measured_traffic(N, T, len(sizes), args.dtype, args.shared, "fused" if fused else "pipe") \
-        if args.workload == "cfg3" else (None, None)
+    traffic, traffic_src = measured_traffic(N if args.workload == "cfg3" else "U(256,2048)", T, len(sizes),
+                                            args.dtype, args.shared, "fused" if fused else "pipe")
 
     # the reference's precision at the metric's shape (model.py:280-316 computes in fp32), and the
     # one-bag-per-call caller (infer.py:187-191): N = 1 only, after the headline's timed steps

@@ -179,7 +179,10 @@ int cu_count() {
 }
 
 #ifndef MCGMIL_DMA_DIAG
-#define MCGMIL_DMA_DIAG 0          // conv_dma_kernel timing diagnostics (wrong results): 1 no DMA wait
+// conv_dma_kernel timing diagnostics (wrong results; after the first NS steps): 1 no DMA wait,
+// 2 no barrier, 4 no MFMAs (fragments still read), 8 no fragment reads (MFMAs on register junk),
+// 16 no DMA issued
+#define MCGMIL_DMA_DIAG 0
 #endif
 
 // ---- BatchNorm statistics of the output (see the header comment)
@@ -397,20 +400,37 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
             const int kq = ks * 4 + (lane >> 4);
             bf16x8 wf[FI];
 #pragma unroll
-            for (int i = 0; i < FI; ++i)
+            for (int i = 0; i < FI; ++i) {
+#if MCGMIL_DMA_DIAG & 8
+                asm volatile("" : "=v"(wf[i]));
+#else
                 wf[i] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WN + i * 16 + (lane & 15), kq));
+#endif
+            }
             // pixel fragments in groups of 4 (fewer live operand registers with 8 of them)
 #pragma unroll
             for (int j0 = 0; j0 < FJ; j0 += 4) {
                 bf16x8 xf[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < 4; ++j) {
+#if MCGMIL_DMA_DIAG & 8
+                    asm volatile("" : "=v"(xf[j]));
+#else
                     xf[j] = *reinterpret_cast<const bf16x8*>(A + swz(wm * WM + (j0 + j) * 16 + (lane & 15), kq));
+#endif
+                }
+#if MCGMIL_DMA_DIAG & 4
+#pragma unroll
+                for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(xf[j]));
+#pragma unroll
+                for (int i = 0; i < FI; ++i) asm volatile("" ::"v"(wf[i]));
+#else
 #pragma unroll
                 for (int i = 0; i < FI; ++i)
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
                         acc[j0 + j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[j0 + j][i], 0, 0, 0);
+#endif
             }
         }
     };
@@ -442,9 +462,16 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
             if (NS == 3 && s + 1 < steps) wait_vmcnt<PA + PB>();
             else wait_vmcnt<0>();
         }
+#if MCGMIL_DMA_DIAG & 2
+        if (s < NS)
+#endif
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+#if MCGMIL_DMA_DIAG & 16
+        if (s + NS - 1 < steps && s < NS) issue(buf == 0 ? NS - 1 : buf - 1);
+#else
         if (s + NS - 1 < steps) issue(buf == 0 ? NS - 1 : buf - 1);
+#endif
         compute(buf);
         buf = buf == NS - 1 ? 0 : buf + 1;
         if (++kt == g.KT) {

@@ -19,7 +19,7 @@ for spec in "$@"; do
     # per source, as mcgmil/_build.py: the gate kernels (mcgmil.hip) with the max-ILP scheduler
     (
         objs=""
-        srcs="mcgmil.hip mcgmil_fused.hip mcgmil_image.hip mcgmil_bn.hip mcgmil_conv.hip mcgmil_stem.hip mcgmil_conv32.hip"
+        srcs="mcgmil.hip mcgmil_fused.hip mcgmil_image.hip mcgmil_bn.hip mcgmil_conv.hip mcgmil_stem.hip mcgmil_conv32.hip mcgmil_calib.hip"
         [ -n "${GATE_ONLY:-}" ] && srcs="mcgmil.hip mcgmil_fused.hip"   # gate-kernel A/B: the MCDO entry points only
         for f in $srcs; do
             [ -f "$src/$f" ] || continue

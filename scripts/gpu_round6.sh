@@ -46,6 +46,10 @@ for s in ${STEPS:-smoke calib all bench}; do
         grbm4) rm -rf "$OUT/grbm4"; step grbm4 300 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace -d "$OUT/grbm4" -o run --output-format csv -- python3 bench.py --workload cfg4 --steps 5 --warmup 2 --no-cpu-baseline --busy-seconds 4
               python3 scripts/grbm_clock.py "$OUT/grbm4" > "$OUT/grbm4_clock.json"; head -30 "$OUT/grbm4_clock.json" ;;
         cfg5drift) step pytest_cfg5drift 400 python -u -m pytest tests/test_gpu_pipeline.py -m gpu -x -q -s -rf --timeout 300 --timeout-method thread -k cfg5 ;;
+        pmcfinal) step pmc_final 700 env PMC_OUT=gpurun_out/pmc_final PMC_CMD="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --busy-seconds 0 --no-secondary --no-calibration" PASSES="fetch write" bash scripts/pmc_passes.sh
+              python3 scripts/traffic_json.py gpurun_out/pmc_final gpurun_out/gate_traffic.json cfg3 "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-trace -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --busy-seconds 0 --no-secondary --no-calibration (scripts/pmc_passes.sh PASSES='fetch write')" ;;
+        pmc4) step pmc_cfg4 700 env PMC_OUT=gpurun_out/pmc_cfg4 PMC_CMD="python3 bench.py --workload cfg4 --steps 2 --warmup 1 --no-cpu-baseline --busy-seconds 0 --no-calibration" PASSES="fetch write" bash scripts/pmc_passes.sh
+              python3 scripts/traffic_json.py gpurun_out/pmc_cfg4 gpurun_out/gate_traffic_cfg4.json cfg4 "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-trace -- python3 bench.py --workload cfg4 --steps 2 --warmup 1 --no-cpu-baseline --busy-seconds 0 --no-calibration (scripts/pmc_passes.sh PASSES='fetch write')" ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         fusednew) step pytest_fusednew 600 python -u -m pytest tests/test_gpu_fused.py -m gpu -x -v --timeout 300 --timeout-method thread -k "xcd or bench_step or path_flag" ;;
         cfg4full) step pytest_cfg4full 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 400 --timeout-method thread -k "cfg4_full" ;;
