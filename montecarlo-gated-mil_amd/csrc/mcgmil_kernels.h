@@ -817,6 +817,26 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
     MCGMIL_STAMP(p, 7);
 }
 
+// XCD-aware tile order of the two-kernel gate launches (guide T1, bijective form): workgroup b runs
+// logical tile xcd_tile(b, n). Workgroups are dealt to the 8 XCDs round-robin (b % 8), so each XCD
+// gets one contiguous chunk of the (bag, t, n)-ordered tiles: all T samples of a bag run on one
+// XCD and re-read its H rows from that XCD's L2. With the identity order a ragged bag's tile
+// boundaries shift from sample to sample, each XCD saw every bag, and config 4's launch fetched
+// 3.7x its algorithmic bytes (profiles/r06/gate_traffic_cfg4.json). Every tile's arithmetic is
+// unchanged, so outputs are bitwise the same. MCGMIL_XCD_TILES=0 (A/B builds): identity order.
+#ifndef MCGMIL_XCD_TILES
+#define MCGMIL_XCD_TILES 1
+#endif
+__device__ __forceinline__ long long xcd_tile(unsigned b, unsigned n) {
+#if MCGMIL_XCD_TILES
+    const unsigned x = b & 7u, q = n >> 3, r = n & 7u;
+    return (long long)((x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3));
+#else
+    (void)n;
+    return (long long)b;
+#endif
+}
+
 template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS, bool PROBE = false>
 __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -825,7 +845,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     float* red = reinterpret_cast<float*>(smem + (size_t)pipe_slots<E>() * BM * 32 * sizeof(E));
     float* zred = red + red_floats<BM, MAXC>();
     int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);
-    const long long R0 = (long long)blockIdx.x * BM;
+    const long long R0 = xcd_tile(blockIdx.x, gridDim.x) * BM;
 
     if constexpr (PROBE) clock_probe(p, 0);
     MCGMIL_STAMP(p, 0);
