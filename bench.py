@@ -61,6 +61,18 @@ def measured_traffic(N, T, B, dtype, shared, path_kind):
     return None, None
 
 
+def measured_grbm_clock(workload, kernel):
+    """The product launch's clock from the newest committed GRBM pass of this workload
+    (profiles/r*/grbm_clock_<workload>.json, scripts/grbm_clock.py: GRBM_GUI_ACTIVE / 8 / dispatch
+    wall, median over the timed dispatches of `kernel`, the unprobed instantiation)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", f"grbm_clock_{workload}.json")), reverse=True):
+        for name, rec in json.load(open(path)).items():
+            if kernel in name and not name.endswith("true>(mcgmil::GateParams)") and "Lb1EEEv" not in name:
+                return rec["grbm_clock_mhz_median"], os.path.relpath(path, REPO)
+    return None, None
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -291,7 +303,8 @@ def main():
                          # pooling) when fused, the gate GEMM kernel alone otherwise
                          "timed_path": "fused: gate+softmax+pooling" if fused else "two-kernel: gate only",
                          "kernel_ms": gate_ms, "algorithmic_tflop_per_launch": F / 1e12,
-                         **at_clock(achieved, PEAK_TFLOPS[args.dtype], r["clock"], args.dtype)},
+                         **at_clock(achieved, PEAK_TFLOPS[args.dtype], r["clock"], args.dtype),
+                         **grbm_keys(achieved, PEAK_TFLOPS[args.dtype], args.workload, fused)},
             "roofline_hbm": {"achieved": hbm_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": hbm_gbs / PEAK_HBM_GBS,
                              "algorithmic_bytes_per_launch": hbm_bytes},
@@ -540,6 +553,19 @@ def vs_measured(achieved, dtype, clock_mhz=None):
     if clock_mhz and c["clock_mhz"]:
         out["per_clock_frac_of_measured"] = (achieved / clock_mhz) / (c["tflops"] / c["clock_mhz"])
     return out
+
+
+def grbm_keys(achieved, peak, workload, fused):
+    """The cross-check of the in-kernel clock: the probed launch runs the PROBE instantiation, whose
+    code differs from the product kernel's (measured 11% slower, at a ~9% higher clock under
+    rocprofv3, profiles/r06/grbm_clock_cfg3.json), so frac_at_clock uses a clock the product launch
+    does not hold. The committed GRBM pass gives the product dispatches' own clock."""
+    mhz, src = measured_grbm_clock(workload, "gate_fused_kernel" if fused else "gate_pipe_kernel")
+    if mhz is None:
+        return {}
+    return {"clock_mhz_grbm": mhz, "frac_at_grbm_clock": achieved / (peak * mhz / MAX_CLOCK_MHZ),
+            "grbm_source": f"{src} (GRBM_GUI_ACTIVE / 8 / dispatch wall, timed dispatches, a committed "
+                           f"rocprofv3 pass of this workload)"}
 
 
 def shared_secondary(args, dev, steps=10, warmup=3):
