@@ -276,7 +276,7 @@ __global__ __launch_bounds__(kPPThreads, 2) void gate_pp_kernel(const GateParams
     constexpr int BM = 16 * RT;
     int* rinfo = reinterpret_cast<int*>(smem + (size_t)2 * RT * 64 * 8 * sizeof(E) +
                                         ((size_t)kPPWaves * MAXC * 4 * BM + (size_t)MAXC * BM) * 4);
-    const long long R0 = xcd_tile(blockIdx.x, gridDim.x) * BM;   // XCD-aware order (mcgmil_kernels.h)
+    const long long R0 = xcd_tile(blockIdx.x, gridDim.x, p.B) * BM;   // XCD-aware order (mcgmil_kernels.h)
     if constexpr (PROBE) clock_probe(p, 0);
     MCGMIL_STAMP(p, 0);
     fill_row_table<BM>(p, R0, rinfo);

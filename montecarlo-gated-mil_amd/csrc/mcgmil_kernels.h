@@ -823,16 +823,21 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
 // XCD and re-read its H rows from that XCD's L2. With the identity order a ragged bag's tile
 // boundaries shift from sample to sample, each XCD saw every bag, and config 4's launch fetched
 // 3.7x its algorithmic bytes (profiles/r06/gate_traffic_cfg4.json). Every tile's arithmetic is
-// unchanged, so outputs are bitwise the same. MCGMIL_XCD_TILES=0 (A/B builds): identity order.
+// unchanged, so outputs are bitwise the same. Batches of fewer than 8 bags keep the identity
+// order: there a chunk would make every XCD read the whole bag, and the one-bag-per-call path
+// measured 1-3% slower with it (profiles/r06/xcd_tiles/). MCGMIL_XCD_TILES=0 (A/B builds):
+// identity order always.
 #ifndef MCGMIL_XCD_TILES
 #define MCGMIL_XCD_TILES 1
 #endif
-__device__ __forceinline__ long long xcd_tile(unsigned b, unsigned n) {
+__device__ __forceinline__ long long xcd_tile(unsigned b, unsigned n, int bags) {
 #if MCGMIL_XCD_TILES
     const unsigned x = b & 7u, q = n >> 3, r = n & 7u;
-    return (long long)((x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3));
+    const unsigned l = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+    return (long long)(bags >= 8 ? l : b);
 #else
     (void)n;
+    (void)bags;
     return (long long)b;
 #endif
 }
@@ -845,7 +850,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     float* red = reinterpret_cast<float*>(smem + (size_t)pipe_slots<E>() * BM * 32 * sizeof(E));
     float* zred = red + red_floats<BM, MAXC>();
     int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);
-    const long long R0 = xcd_tile(blockIdx.x, gridDim.x) * BM;
+    const long long R0 = xcd_tile(blockIdx.x, gridDim.x, p.B) * BM;
 
     if constexpr (PROBE) clock_probe(p, 0);
     MCGMIL_STAMP(p, 0);
