@@ -178,6 +178,11 @@ def run(args, world, rank, dev, peak_tflops, calib=None):
                    "features": ("bf16: HIP backbone (autocast), bf16 head operands" if bf16 else
                                 "fp32: fp32 MFMA convolutions incl. the gather-mode stem + fused BN (HIP, conv32_kernel), fp32 head operands"),
                    "drift_vs_fp32_pipeline": drift,
+                   "drift_note": (None if drift is None else
+                                  "the bf16 line's uncertainty outputs approximate the fp32 (reference-precision) "
+                                  "pipeline: A_var ~4% nrel, A_mean ~1%, the same as PyTorch-ROCm's own bf16 autocast "
+                                  "pipeline on this bag (tests/test_gpu_pipeline.py bounds this build by 1.25x of it; "
+                                  "DESIGN.md §7); the fp32 line (--features fp32) is the reference precision"),
                    "stage_ms": stage_ms, "parallelism": f"one image per GPU per step, {world} GPU(s)"},
         "roofline": {"bound": "mfma", "achieved": feat_tflops,
                      "peak": peak_tflops if bf16 else PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
