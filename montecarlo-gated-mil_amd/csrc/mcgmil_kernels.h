@@ -759,7 +759,11 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
             }
 #endif
         }
+#if MCGMIL_DIAG & 128   // ablation (timing only, wrong results): no barrier between K steps
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
         __syncthreads();
+#endif
     };
 
     // bf16 separate heads: the epilogue's head vectors load under the K loop instead of after it
