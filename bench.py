@@ -563,9 +563,13 @@ def grbm_keys(achieved, peak, workload, fused):
     mhz, src = measured_grbm_clock(workload, "gate_fused_kernel" if fused else "gate_pipe_kernel")
     if mhz is None:
         return {}
-    return {"clock_mhz_grbm": mhz, "frac_at_grbm_clock": achieved / (peak * mhz / MAX_CLOCK_MHZ),
-            "grbm_source": f"{src} (GRBM_GUI_ACTIVE / 8 / dispatch wall, timed dispatches, a committed "
-                           f"rocprofv3 pass of this workload)"}
+    out = {"clock_mhz_grbm": mhz, "frac_at_grbm_clock": achieved / (peak * mhz / MAX_CLOCK_MHZ),
+           "grbm_source": f"{src} (GRBM_GUI_ACTIVE / 8 / dispatch wall, timed dispatches, a committed "
+                          f"rocprofv3 pass of this workload)"}
+    c = CALIB.get("bf16" if peak == PEAK_TFLOPS["bf16"] else "f32")
+    if c and c.get("clock_mhz"):
+        out["per_clock_frac_of_measured_grbm"] = (achieved / mhz) / (c["tflops"] / c["clock_mhz"])
+    return out
 
 
 def shared_secondary(args, dev, steps=10, warmup=3):
