@@ -311,7 +311,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
     constexpr int FI = WN / 16, FJ = WM / 16;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: LDS-DMA bases (M0) by SALU
     const int L = xcd_remap((int)blockIdx.x, (int)gridDim.x);
     const int tn = L % g.tiles_n, gm = L / g.tiles_n;
     const int tm0 = (int)((long long)gm * g.tiles_m / g.Gm);
@@ -330,10 +330,12 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
     }
     // A pieces: the pixel rows of the tile being fetched (the issue side runs two steps ahead)
     int itm = -1;
-    // per piece: the window origin as a pixel index (may be negative) and the origin (ih0, iw0) as
-    // two int16 halves for the bounds test; the source chunk of the lane's LDS slot is the same
-    // for every piece ((r >> 1) & 7 does not depend on j)
-    int org[PA], ohw[PA];
+    // per piece, fixed for a tile: the byte offset of the window origin's source chunk (the pixel
+    // index may be negative: a valid tap adds a non-negative total) and a bit per (kh, kw) tap that
+    // lies inside the image (KH * KW <= 49, host-checked), so a K step's piece costs an add and a
+    // bit test -- no multiply and no bounds arithmetic per step. The source chunk of the lane's LDS
+    // slot is the same for every piece ((r >> 1) & 7 does not depend on j).
+    uint32_t orgb[PA], mlo[PA], mhi[PA];
     const int cha = ((lane & 7) ^ ((4 * wave + (lane >> 4)) & 7)) * 8;
     auto setup = [&](int tm) {
         itm = tm;
@@ -345,10 +347,16 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
             const int n = mm / (g.OH * g.OW);
             const int rem = mm - n * g.OH * g.OW;
             const int oh = rem / g.OW, ow = rem - oh * g.OW;
-            const int ih0 = m < g.M ? oh * g.stride - g.pad : -16384;   // rows past M load zeros
-            const int iw0 = ow * g.stride - g.pad;
-            org[j] = n * g.H * g.W + ih0 * g.W + iw0;
-            ohw[j] = (int)(((uint32_t)ih0 << 16) | ((uint32_t)iw0 & 0xFFFFu));
+            const int ih0 = oh * g.stride - g.pad, iw0 = ow * g.stride - g.pad;
+            orgb[j] = (uint32_t)(((n * g.H + ih0) * g.W + iw0) * g.Cin + cha) * 2u;
+            uint32_t cols = 0;
+            for (int kw = 0; kw < g.KW; ++kw) cols |= ((unsigned)(iw0 + kw) < (unsigned)g.W ? 1u : 0u) << kw;
+            uint64_t taps = 0;
+            if (m < g.M)                                                  // rows past M load zeros
+                for (int kh = 0; kh < g.KH; ++kh)
+                    if ((unsigned)(ih0 + kh) < (unsigned)g.H) taps |= (uint64_t)cols << (kh * g.KW);
+            mlo[j] = (uint32_t)taps;
+            mhi[j] = (uint32_t)(taps >> 32);
         }
     };
     // issue() is called for consecutive steps: its (tile, K tile) cursor advances by one per call --
@@ -368,15 +376,14 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
             i_kt = i_cc = i_kw = i_kh = 0;
             ++i_tm;
         }
-        const int koff = kh * g.W + kw;
+        const uint32_t koffb = (uint32_t)(((kh * g.W + kw) * g.Cin + cc * 64) * 2);   // wave-uniform
+        const int tap = kh * g.KW + kw;
         unsigned char* A = smem + buf * STAGE;
         unsigned char* B = A + BM * kRowBytes;
 #pragma unroll
         for (int j = 0; j < PA; ++j) {
-            const int ih = (ohw[j] >> 16) + kh, iw = (int)(short)(ohw[j] & 0xFFFF) + kw;
-            const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-            const uint32_t off = ((uint32_t)(org[j] + koff) * (uint32_t)g.Cin + (uint32_t)(cc * 64 + cha)) * 2u;
-            dma16(xr, A + (wave + 8 * j) * 1024, ok ? off : 0x80000000u, 0);
+            const bool ok = (((tap < 32 ? mlo[j] : mhi[j]) >> (tap & 31)) & 1u) != 0u;
+            dma16(xr, A + (wave + 8 * j) * 1024, ok ? orgb[j] + koffb : 0x80000000u, 0);
         }
 #pragma unroll
         for (int j = 0; j < PB; ++j)
@@ -1006,7 +1013,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
     constexpr int BN = 128, WGM = 4, WGN = 2, WM = 64, WN = 64, FI = 4, FJ = 4;
     constexpr size_t PATCH = (size_t)kPatchPx * kRowBytes, WSTAGE = (size_t)BN * kRowBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: LDS-DMA bases (M0) by SALU
     const int wm = wave / WGN, wn = wave % WGN;
     const int L = xcd_remap((int)blockIdx.x, (int)gridDim.x);
     const int tn = L % g.tiles_n, gm = L / g.tiles_n;
