@@ -47,10 +47,12 @@
 extern "C" {
 #endif
 
-#define MCGMIL_ABI_VERSION 5   /* 2: mcgmil_args.flags (path selection); 3: mcgmil_conv_args.flags,
+#define MCGMIL_ABI_VERSION 6   /* 2: mcgmil_args.flags (path selection); 3: mcgmil_conv_args.flags,
                                   mcgmil_stem_args.flags (mcgmil_features.h); 4: MCGMIL_CLOCK_PROBE (and a
                                   row-gate flag); 5: the row-gate flag (3 << 2) and its weight stream in the
-                                  packed weights removed -- measured slower everywhere, DESIGN.md §5 */
+                                  packed weights removed -- measured slower everywhere, DESIGN.md §5;
+                                  6: mcgmil_conv_args.workspace / workspace_bytes and
+                                  mcgmil_conv_workspace_size (the convolutions' K split) */
 
 enum mcgmil_status {
     MCGMIL_OK = 0,

@@ -116,9 +116,18 @@ typedef struct mcgmil_conv_args {
                                    writing and re-reading bn(x). Only where
                                    mcgmil_conv_input_bn() reports support (the 3x3 / stride 1 halo
                                    kernels), else MCGMIL_E_UNSUPPORTED. NULL: x as is */
-    int32_t flags;              /* mcgmil_conv_flags: the kernel shape (0 = auto; performance only,
-                                   every shape computes the same sums; MCGMIL_CONV_TILE in the
-                                   environment -- nohalo | small | big512 -- overrides) */
+    void* workspace;            /* optional device scratch, 256-byte aligned, of
+                                   mcgmil_conv_workspace_size() bytes (0 for most layers). With it
+                                   a layer whose last round of 256 x 256 pixel tiles would leave
+                                   most CUs idle cuts those tiles' K loop into 2-4 ranges (fp32
+                                   sums added in range order, then one rounding to bf16 -- within
+                                   the fp32 accumulation bound of the whole-tile sums, not bitwise
+                                   them). NULL or smaller: whole tiles. mcgmil_conv2d_f32 ignores it */
+    size_t workspace_bytes;
+    int32_t flags;              /* mcgmil_conv_flags: the kernel shape (0 = auto; performance only;
+                                   every shape sums each output's K terms in the same order, so
+                                   they agree bitwise where no K split applies; MCGMIL_CONV_TILE in
+                                   the environment -- nohalo | small | big512 -- overrides) */
     int32_t reserved;           /* must be 0 */
 } mcgmil_conv_args;
 
@@ -185,6 +194,9 @@ int mcgmil_pack_stem_weights(const mcgmil_stem_args* a, const void* weight, int3
 int mcgmil_stem_workspace_size(const mcgmil_stem_args* a, size_t* bytes);
 int mcgmil_stem_forward(const mcgmil_stem_args* a, void* stream);
 int mcgmil_conv_stats_parts(const mcgmil_conv_args* a, int32_t* parts);
+/* Bytes of mcgmil_conv_args.workspace this layer's plan can use (0: none). Replaces nothing in the
+ * reference (torch.nn.Conv2d allocates its own scratch through the caching allocator). */
+int mcgmil_conv_workspace_size(const mcgmil_conv_args* a, size_t* bytes);
 /* *supported = 1 when mcgmil_conv2d accepts in_ab for this geometry (in_ab itself not read) */
 int mcgmil_conv_input_bn(const mcgmil_conv_args* a, int32_t* supported);
 int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream);

@@ -72,6 +72,14 @@ struct ConvGeom {
     int Gm;              // workgroups per channel tile
     uint32_t x_bytes;    // buffer range of x (< 2^31, host-checked)
     uint32_t w_bytes;
+    // K split of the last pixel tiles (conv_dma_kernel without statistics, split_p >= 2): each
+    // workgroup row gm runs full_tiles whole tiles [gm F, (gm + 1) F); the R = tiles_m - F Gm tiles
+    // left are cut into split_p K ranges, range p of left tile q run by row q split_p + p, which
+    // stores its fp32 sums in part[(tn R + q) split_p + p][BM][BN]; conv_split_fixup_kernel adds
+    // the ranges in order and rounds once
+    float* part;
+    int split_p;         // 0: no split
+    int full_tiles;      // F
 };
 
 // byte offset of 16-byte chunk c of row r in a swizzled [rows][128 B] stage: rows 2j and 2j+1
@@ -183,6 +191,12 @@ int cu_count() {
 // 2 no barrier, 4 no MFMAs (fragments still read), 8 no fragment reads (MFMAs on register junk),
 // 16 no DMA issued
 #define MCGMIL_DMA_DIAG 0
+#endif
+#ifndef MCGMIL_HALO_DIAG
+// conv3x3_halo_kernel timing diagnostics (wrong results; after the first 2 steps): 1 no DMA wait,
+// 2 no barrier, 4 no MFMAs (fragments still read), 8 no fragment reads, 16 no input-BatchNorm
+// rewrite (XF), 32 no DMA issued
+#define MCGMIL_HALO_DIAG 0
 #endif
 
 // ---- BatchNorm statistics of the output (see the header comment)
@@ -314,9 +328,24 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: LDS-DMA bases (M0) by SALU
     const int L = xcd_remap((int)blockIdx.x, (int)gridDim.x);
     const int tn = L % g.tiles_n, gm = L / g.tiles_n;
-    const int tm0 = (int)((long long)gm * g.tiles_m / g.Gm);
-    const int tm1 = (int)((long long)(gm + 1) * g.tiles_m / g.Gm);
-    const int steps = (tm1 - tm0) * g.KT;
+    int tm0 = (int)((long long)gm * g.tiles_m / g.Gm);
+    int tm1 = (int)((long long)(gm + 1) * g.tiles_m / g.Gm);
+    // K split (STATS off, host-checked): whole tiles, then at most one K range of a left tile
+    bool piece = false;
+    int ptm = 0, k0 = 0, k1 = 0, pslot = 0;
+    if (!STATS && g.split_p > 0) {
+        tm0 = gm * g.full_tiles;
+        tm1 = tm0 + g.full_tiles;
+        const int R = g.tiles_m - g.full_tiles * g.Gm, q = gm / g.split_p, pp = gm - q * g.split_p;
+        if (q < R) {
+            piece = true;
+            ptm = g.full_tiles * g.Gm + q;
+            k0 = pp * g.KT / g.split_p;
+            k1 = (pp + 1) * g.KT / g.split_p;
+            pslot = (tn * R + q) * g.split_p + pp;
+        }
+    }
+    const int steps = (tm1 - tm0) * g.KT + (piece ? k1 - k0 : 0);
     const __amdgpu_buffer_rsrc_t xr = make_rsrc(g.x, g.x_bytes);
     const __amdgpu_buffer_rsrc_t wr = make_rsrc(g.w, g.w_bytes);
     const uint32_t K = (uint32_t)(g.KH * g.KW * g.Cin);
@@ -362,6 +391,15 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
     // issue() is called for consecutive steps: its (tile, K tile) cursor advances by one per call --
     // kt = (kh * KW + kw) * cin_tiles + cc -- without a runtime division per step
     int i_tm = tm0, i_kt = 0, i_cc = 0, i_kw = 0, i_kh = 0;
+    auto to_piece = [&]() {            // the issue cursor jumps to (ptm, k0)
+        i_tm = ptm;
+        i_kt = k0;
+        i_cc = k0 % g.cin_tiles;
+        const int t = k0 / g.cin_tiles;
+        i_kw = t % g.KW;
+        i_kh = t / g.KW;
+    };
+    if (piece && tm0 == tm1) to_piece();
     auto issue = [&](int buf) {
         if (i_tm != itm) setup(i_tm);
         const int kt = i_kt, cc = i_cc, kh = i_kh, kw = i_kw;
@@ -375,6 +413,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
         if (++i_kt == g.KT) {
             i_kt = i_cc = i_kw = i_kh = 0;
             ++i_tm;
+            if (piece && i_tm == tm1) to_piece();     // the last whole tile's K steps all issued
         }
         const uint32_t koffb = (uint32_t)(((kh * g.W + kw) * g.Cin + cc * 64) * 2);   // wave-uniform
         const int tap = kh * g.KW + kw;
@@ -441,6 +480,19 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
             }
         }
     };
+    // a K range of a left tile: fp32 sums to part[pslot] ([BM][BN], 4 channels per 16-B store)
+    auto store_part = [&]() {
+        float* dst = g.part + (size_t)pslot * BM * BN + wn * WN + 4 * (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+            const int ml = wm * WM + j * 16 + (lane & 15);
+#pragma unroll
+            for (int i = 0; i < FI; ++i) {
+                *reinterpret_cast<f32x4*>(dst + (size_t)ml * BN + i * 16) = acc[j][i];
+                acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    };
     auto epilogue = [&](int tm, bool first) {
         const bool full = (tm + 1) * BM <= g.M;
 #pragma unroll
@@ -459,7 +511,14 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
         issue(0);
         if (NS == 3 && steps > 1) issue(1);
     }
-    int buf = 0, kt = 0, tm = tm0;
+    int buf = 0, kt = 0, tm = tm0, kend = g.KT;
+    bool in_piece = false;
+    if (piece && tm0 == tm1) {
+        in_piece = true;
+        tm = ptm;
+        kt = k0;
+        kend = k1;
+    }
     for (int s = 0; s < steps; ++s) {
         // step s landed (counted: the next step's DMAs may stay in flight; vmcnt retires in order)
 #if MCGMIL_DMA_DIAG & 1   // timing only: no wait for the stage's DMA after the first steps (wrong results)
@@ -481,14 +540,53 @@ __global__ __launch_bounds__(kThreads, 1) void conv_dma_kernel(const ConvGeom g)
 #endif
         compute(buf);
         buf = buf == NS - 1 ? 0 : buf + 1;
-        if (++kt == g.KT) {
-            epilogue(tm, tm == tm0);
-            kt = 0;
-            ++tm;
+        if (++kt == kend) {
+            if (in_piece) {
+                store_part();
+            } else {
+                epilogue(tm, tm == tm0);
+                kt = 0;
+                ++tm;
+                if (piece && tm == tm1) {
+                    in_piece = true;
+                    tm = ptm;
+                    kt = k0;
+                    kend = k1;
+                }
+            }
         }
     }
     if (STATS) write_stats<4 * FI, WGM, BN>(st, wn * WN, wm, reinterpret_cast<float*>(smem), g.stats, gm,
                                              g.Cout, tn * BN);
+}
+
+// The K split's second pass (ConvGeom::split_p): one thread per (left tile pixel, 8 channels) adds
+// the tile's split_p fp32 K-range sums in range order and rounds once to bf16 -- the split tile's
+// outputs differ from the unsplit kernel's only in where the fp32 sum is rounded.
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_split_fixup_kernel(const ConvGeom g) {
+    const int R = g.tiles_m - g.full_tiles * g.Gm, P = g.split_p;
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long long)R * g.tiles_n * BM * (BN / 8)) return;
+    const int cg = (int)(idx % (BN / 8));
+    const long long r = idx / (BN / 8);
+    const int ml = (int)(r % BM), t = (int)(r / BM);            // t = tn R + q
+    const int tn = t / R, q = t - tn * R;
+    const int m = (g.full_tiles * g.Gm + q) * BM + ml;
+    if (m >= g.M) return;
+    const float* src = g.part + (size_t)t * P * BM * BN + (size_t)ml * BN + cg * 8;
+    f32x4 a = *reinterpret_cast<const f32x4*>(src), b = *reinterpret_cast<const f32x4*>(src + 4);
+    for (int p = 1; p < P; ++p) {
+        a += *reinterpret_cast<const f32x4*>(src + (size_t)p * BM * BN);
+        b += *reinterpret_cast<const f32x4*>(src + (size_t)p * BM * BN + 4);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        o[v] = (__bf16)a[v];
+        o[4 + v] = (__bf16)b[v];
+    }
+    *reinterpret_cast<bf16x8*>(g.y + (size_t)m * g.Cout + tn * BN + cg * 8) = o;
 }
 
 // ---- 3x3 / stride 1 / pad 1, 64 -> 64 channels (ResNet layer 1): halo-tile kernel.
@@ -1170,11 +1268,15 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
     int tm = tm0, r = 0, pbuf = 0;     // r = step within the tile
     int wait_kind = 0;                 // 0: vmcnt(0), 1: a patch piece after the weights, 2: stores
     for (int s = 0; s < steps; ++s) {
-        if (wait_kind == 1) wait_vmcnt<1>();
-        else if (wait_kind == 2) wait_vmcnt<FI * FJ>();
-        else wait_vmcnt<0>();
+        constexpr int D = MCGMIL_HALO_DIAG;
+        const bool live = s < 2;            // the diagnostics keep the first steps intact
+        if (!(D & 1) || live) {
+            if (wait_kind == 1) wait_vmcnt<1>();
+            else if (wait_kind == 2) wait_vmcnt<FI * FJ>();
+            else wait_vmcnt<0>();
+        }
         const int cc = r / 9, tap = r - cc * 9;
-        if (XF && tap == 0) {       // this step opens a patch: the rest of this lane's slots
+        if (XF && tap == 0 && (!(D & 16) || live)) {       // this step opens a patch: the rest of this lane's slots
             if (s == 0) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) xform(k);
@@ -1183,10 +1285,10 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
             }
             wait_lds_writes();
         }
-        __builtin_amdgcn_s_barrier();
+        if (!(D & 2) || live) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         wait_kind = 0;
-        if (s + 1 < steps) issue_w(r + 1 == SPT ? 0 : r + 1, (s + 1) & 1);
+        if (s + 1 < steps && (!(D & 32) || live)) issue_w(r + 1 == SPT ? 0 : r + 1, (s + 1) & 1);
         // the next (tile, cc) patch: begun at tap 0, one piece per tap 0..7
         const bool more_patch = (r + 9 < SPT) || (tm + 1 < tm1);
         if (more_patch && tap < 8) {
@@ -1196,7 +1298,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
             }
             // vmcnt(1) at the next step leaves only this piece in flight; without a piece the
             // weights just issued must land: vmcnt(0)
-            if (patch_piece(tap)) wait_kind = 1;
+            if ((!(D & 32) || live) && patch_piece(tap)) wait_kind = 1;
         }
         // compute step s: A from the patch at the tap offset, B from the weight stage
         {
@@ -1214,12 +1316,26 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
                 const int kq = ks * 4 + (lane >> 4);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int i = 0; i < FI; ++i)
-                    wf[ks][i] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WN + i * 16 + (lane & 15), kq));
+                for (int i = 0; i < FI; ++i) {
+                    if constexpr ((D & 8) != 0) asm volatile("" : "=v"(wf[ks][i]));
+                    else wf[ks][i] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WN + i * 16 + (lane & 15), kq));
+                }
 #pragma unroll
-                for (int j = 0; j < FJ; ++j)
-                    xf[ks][j] = *reinterpret_cast<const bf16x8*>(A + (ks ? ad[j] ^ 64u : ad[j]));
+                for (int j = 0; j < FJ; ++j) {
+                    if constexpr ((D & 8) != 0) asm volatile("" : "=v"(xf[ks][j]));
+                    else xf[ks][j] = *reinterpret_cast<const bf16x8*>(A + (ks ? ad[j] ^ 64u : ad[j]));
+                }
                 if (ks == 0) continue;
+                if constexpr ((D & 4) != 0) {
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                        for (int i = 0; i < FI; ++i) asm volatile("" ::"v"(wf[h][i]));
+#pragma unroll
+                        for (int j = 0; j < FJ; ++j) asm volatile("" ::"v"(xf[h][j]));
+                    }
+                    continue;
+                }
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     if (h == 1) __builtin_amdgcn_sched_barrier(0);
@@ -1233,7 +1349,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_halo_kernel(const HaloGeo
             __builtin_amdgcn_sched_barrier(0);
         }
         // XF: piece tap - 2 of the patch being loaded has landed (the wait above retired it)
-        if (XF && more_patch && tap >= 2) xform(tap - 2);
+        if (XF && more_patch && tap >= 2 && (!(D & 16) || live)) xform(tap - 2);
         if (tap == 8) pbuf ^= 1;                        // next cc (or tile) uses the other patch
         if (++r == SPT) {
             const bool full = (tm + 1) * kBM <= g.M, first = tm == tm0;
@@ -1398,6 +1514,7 @@ struct Plan {
     int parts = 0;         // statistics rows
     size_t lds = 0;
     HaloGeom hg;
+    size_t part_bytes = 0; // K split (kind 6): the fp32 range sums (mcgmil_conv_args.workspace)
 };
 
 ConvGeom geom_of(const mcgmil_conv_args* a) {
@@ -1435,7 +1552,7 @@ int tile_policy(int flags) {
     return env >= 0 ? env : flags;
 }
 
-Plan make_plan(ConvGeom& g, int flags) {
+Plan make_plan(ConvGeom& g, int flags, bool split_ok = false) {
     Plan p;
     const int cus = cu_count();
     const int policy = tile_policy(flags);
@@ -1556,6 +1673,20 @@ Plan make_plan(ConvGeom& g, int flags) {
         g.Gm = gb;
         p.kind = bn == 256 ? 6 : 5;
         p.grid = g.tiles_n * gb;
+        // tiles_m = F gb + R, 0 < R: the last round of tiles runs on R of gb workgroup rows. With
+        // a workspace those R tiles are cut into P = gb / R K ranges (at most 4, each >= 4 K steps),
+        // so every row runs F tiles + at most 1 / P of one: layer 4 of config 5 (289 tiles per 128
+        // rows, 3 tile times -> 2.33)
+        if (split_ok && p.kind == 6) {
+            const int F = g.tiles_m / gb, R = g.tiles_m - F * gb;
+            int P = R > 0 ? gb / R : 0;
+            if (P > 4) P = 4;
+            if (F >= 1 && P >= 2 && g.KT >= 4 * P) {
+                g.split_p = P;
+                g.full_tiles = F;
+                p.part_bytes = (size_t)R * g.tiles_n * P * bm * bn * sizeof(float);
+            }
+        }
         // no statistics from these shapes: with them the kernel spills (256 VGPRs), and the separate
         // statistics pass of a layer-3/4 activation (10-20 us) costs less than that
         p.parts = 0;
@@ -1611,7 +1742,14 @@ int launch(const ConvGeom& g, const Plan& p, hipStream_t s) {
         return stats ? launch_lds(conv_dma_kernel<256, 128, 4, 3, true>, grid, block, p.lds, s, g)
                      : launch_lds(conv_dma_kernel<256, 128, 4, 3, false>, grid, block, p.lds, s, g);
     if (p.kind == 5) return launch_lds(conv_dma_kernel<512, 128, 4, 2, false>, grid, block, p.lds, s, g);
-    if (p.kind == 6) return launch_lds(conv_dma_kernel<256, 256, 2, 2, false>, grid, block, p.lds, s, g);
+    if (p.kind == 6) {
+        if (int rc = launch_lds(conv_dma_kernel<256, 256, 2, 2, false>, grid, block, p.lds, s, g)) return rc;
+        if (g.split_p == 0) return MCGMIL_OK;
+        const long long n = (long long)(g.tiles_m - g.full_tiles * g.Gm) * g.tiles_n * 256 * (256 / 8);
+        hipLaunchKernelGGL((conv_split_fixup_kernel<256, 256>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "conv_split_fixup_kernel launch");
+    }
     return stats ? launch_lds(conv_dma_kernel<256, 64, 4, 3, true>, grid, block, p.lds, s, g)
                  : launch_lds(conv_dma_kernel<256, 64, 4, 3, false>, grid, block, p.lds, s, g);
 }
@@ -1706,6 +1844,15 @@ int mcgmil_conv_stats_parts(const mcgmil_conv_args* a, int32_t* parts) {
     return MCGMIL_OK;
 }
 
+int mcgmil_conv_workspace_size(const mcgmil_conv_args* a, size_t* bytes) {
+    int rc = validate(a);
+    if (rc) return rc;
+    if (!bytes) return fail(MCGMIL_E_INVALID, "bytes is NULL");
+    ConvGeom g = geom_of(a);
+    *bytes = make_plan(g, a->flags, true).part_bytes;
+    return MCGMIL_OK;
+}
+
 int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream) {
     int rc = validate(a);
     if (rc) return rc;
@@ -1714,8 +1861,14 @@ int mcgmil_conv2d(const mcgmil_conv_args* a, void* stream) {
         return fail(MCGMIL_E_ALIGN, "x, w and y must be 16-byte aligned");
     if ((uintptr_t)a->stats & 3u) return fail(MCGMIL_E_ALIGN, "stats must be 4-byte aligned");
     if ((uintptr_t)a->in_ab & 3u) return fail(MCGMIL_E_ALIGN, "in_ab must be 4-byte aligned");
+    if ((uintptr_t)a->workspace & 255u) return fail(MCGMIL_E_ALIGN, "workspace must be 256-byte aligned");
     ConvGeom g = geom_of(a);
-    const Plan p = make_plan(g, a->flags);
+    Plan p = make_plan(g, a->flags, a->workspace != nullptr);
+    if (p.part_bytes > 0 && a->workspace_bytes < p.part_bytes) {
+        g = geom_of(a);                          // too small for the K split: the whole-tile plan
+        p = make_plan(g, a->flags);
+    }
+    g.part = static_cast<float*>(a->workspace);
     if (a->in_ab && p.kind != 1 && p.kind != 4 && p.kind != 8)
         return fail(MCGMIL_E_UNSUPPORTED, "in_ab: this layer's kernel has no input BatchNorm "
                                           "(see mcgmil_conv_input_bn)");

@@ -18,7 +18,7 @@ MCGMIL_BF16 = 1
 MCGMIL_U8 = 2
 MCGMIL_U16 = 3
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 # mcgmil_args.flags (include/mcgmil.h enum mcgmil_flags)
 PATH_FLAGS = {"auto": 0, "fused": 1, "two_kernel": 2}
 # mcgmil_conv_args.flags / mcgmil_stem_args.flags (include/mcgmil_features.h)
@@ -40,6 +40,7 @@ EXPORTED = (
     "mcgmil_bn_args_size", "mcgmil_bn_workspace_size", "mcgmil_batchnorm_act",
     "mcgmil_batchnorm_coefficients", "mcgmil_conv_input_bn",
     "mcgmil_conv_args_size", "mcgmil_pack_conv_weights", "mcgmil_conv_stats_parts", "mcgmil_conv2d",
+    "mcgmil_conv_workspace_size",
     "mcgmil_conv_packed_size_f32", "mcgmil_pack_conv_weights_f32", "mcgmil_conv2d_f32",
     "mcgmil_conv_stats_parts_f32",
     "mcgmil_stem_args_size", "mcgmil_stem_packed_size", "mcgmil_pack_stem_weights",
@@ -98,6 +99,7 @@ class ConvArgs(ctypes.Structure):
         ("kernel_h", ctypes.c_int32), ("kernel_w", ctypes.c_int32), ("stride", ctypes.c_int32),
         ("pad", ctypes.c_int32), ("in_relu", ctypes.c_int32),
         ("x", _vp), ("w", _vp), ("y", _vp), ("stats", _vp), ("in_ab", _vp),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_size_t),
         ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32),
     ]
 
@@ -219,6 +221,8 @@ def bind(path: str, mcdo_only: bool = False, any_abi: bool = False):
     L.mcgmil_conv_input_bn.restype = ctypes.c_int
     L.mcgmil_conv2d.argtypes = [pc, _vp]
     L.mcgmil_conv2d.restype = ctypes.c_int
+    L.mcgmil_conv_workspace_size.argtypes = [pc, ctypes.POINTER(ctypes.c_size_t)]
+    L.mcgmil_conv_workspace_size.restype = ctypes.c_int
     L.mcgmil_conv_packed_size_f32.argtypes = [pc, ctypes.POINTER(ctypes.c_size_t)]
     L.mcgmil_conv_packed_size_f32.restype = ctypes.c_int
     L.mcgmil_conv_stats_parts_f32.argtypes = [pc, ctypes.POINTER(ctypes.c_int32)]

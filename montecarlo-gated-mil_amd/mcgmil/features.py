@@ -140,6 +140,11 @@ def conv_input_bn(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     return bool(ok.value)
 
 
+def split_enabled() -> bool:
+    """MCGMIL_CONV_SPLIT=0: no K split of the last pixel tiles (mcgmil_conv_args.workspace NULL)."""
+    return os.environ.get("MCGMIL_CONV_SPLIT", "1") != "0"
+
+
 def conv2d(conv: nn.Conv2d, x: torch.Tensor, stats: bool = False,
            in_ab: Optional[torch.Tensor] = None, in_relu: bool = True, flags: int = 0):
     """conv(x) for a channels-last bf16 activation (see conv_fusable) on the MFMA kernel; returns a
@@ -147,7 +152,9 @@ def conv2d(conv: nn.Conv2d, x: torch.Tensor, stats: bool = False,
     as [parts, 3, Cout] (count, mean, M2) blocks for batchnorm_act(..., partials=...), or None
     where the layer's kernel emits none (256 x 256 tiles). With in_ab ([2, Cin] fp32 from
     batchnorm_coefficients) the convolution reads relu?(bn(x)) instead of x (conv_input_bn).
-    flags: mcgmil_conv_args.flags (the tile policy, MCGMIL_CONV_TILE_*; 0 = auto)."""
+    flags: mcgmil_conv_args.flags (the tile policy, MCGMIL_CONV_TILE_*; 0 = auto).
+    Layers whose plan takes a K split of its last tiles get their workspace from the caching
+    allocator (mcgmil_conv_workspace_size); MCGMIL_CONV_SPLIT=0 runs them on whole tiles."""
     if not conv_fusable(conv, x):
         raise ValueError("conv2d needs a CUDA channels-last bf16 activation, a bias-free groups=1 "
                          "convolution with 64k channels and no autograd (see conv_fusable)")
@@ -165,6 +172,13 @@ def conv2d(conv: nn.Conv2d, x: torch.Tensor, stats: bool = False,
                     memory_format=torch.channels_last)
     w = packed_conv_weight(conv, x)
     a.x, a.w, a.y = (ctypes.c_void_p(t.data_ptr()) for t in (x, w, y))
+    ws = None
+    if split_enabled():
+        nb = ctypes.c_size_t()
+        _lib.check(L.mcgmil_conv_workspace_size(ctypes.byref(a), ctypes.byref(nb)), "mcgmil_conv_workspace_size")
+        if nb.value:
+            ws = torch.empty(nb.value, dtype=torch.uint8, device=x.device)   # freed after the launch,
+            a.workspace, a.workspace_bytes = ctypes.c_void_p(ws.data_ptr()), nb.value   # stream-ordered
     part = None
     if stats:
         n = ctypes.c_int32()

@@ -2,7 +2,11 @@
 ResNet-18 layer-3/4 block convolutions of a config-5 bag (PROBE_K instances) in its own process
 (MCGMIL_LIB), saves the outputs, and reports its per-layer time; the parent checks the outputs
 bitwise against the first library. One JSON line per (library, layer) and one verdict line.
-Usage: AB_LIBS=abvar_c/base.so,abvar_c/ph.so python scripts/ab_conv_libs.py"""
+Usage: AB_LIBS=abvar_c/base.so,abvar_c/ph.so python scripts/ab_conv_libs.py
+An entry may add environment settings for its process: lib.so+MCGMIL_CONV_SPLIT=0.
+AB_SET=layer2 runs layer 2's 128 -> 128 3x3 convolution (conv3x3_halo_kernel) instead, plain, with
+BatchNorm statistics, and with statistics + the input BatchNorm (the three launches of a config-5
+image's layer 2)."""
 import json
 import os
 import subprocess
@@ -13,6 +17,15 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # (Cin, H, Cout, k, stride, pad, count in ResNet-18): the Cout % 256 == 0 layers
 LAYERS = [(128, 28, 256, 3, 2, 1, 1), (128, 28, 256, 1, 2, 0, 1), (256, 14, 256, 3, 1, 1, 3),
           (256, 14, 512, 3, 2, 1, 1), (256, 14, 512, 1, 2, 0, 1), (512, 7, 512, 3, 1, 1, 3)]
+# layer 2's halo launches per image: 1 with statistics, 2 with statistics + input BatchNorm
+LAYERS2 = [(128, 28, 128, 3, 1, 1, 0, "plain"), (128, 28, 128, 3, 1, 1, 1, "stats"),
+           (128, 28, 128, 3, 1, 1, 2, "xf")]
+
+
+def layers():
+    if os.environ.get("AB_SET") == "layer2":
+        return LAYERS2
+    return [t + ("plain",) for t in LAYERS]
 
 
 def child(out_dir):
@@ -22,9 +35,9 @@ def child(out_dir):
     from mcgmil.features import conv2d
     dev = torch.device("cuda", 0)
     K = int(os.environ.get("PROBE_K", "1507"))
-    lib = os.path.basename(os.environ["MCGMIL_LIB"])
+    lib = os.path.basename(os.environ["MCGMIL_LIB"]) + os.environ.get("AB_TAG", "")
     tot = 0.0
-    for li, (cin, h, cout, k, s, p, count) in enumerate(LAYERS):
+    for li, (cin, h, cout, k, s, p, count, mode) in enumerate(layers()):
         g = torch.Generator(device=dev).manual_seed(100 + li)
         conv = nn.Conv2d(cin, cout, k, s, p, bias=False).to(dev).eval()
         with torch.no_grad():
@@ -34,22 +47,33 @@ def child(out_dir):
         conv = conv.to(memory_format=torch.channels_last)
         oh = (h + 2 * p - k) // s + 1
         flop = 2.0 * K * oh * oh * cout * cin * k * k
+        kw = {}
+        if mode != "plain":
+            kw["stats"] = True
+        if mode == "xf":
+            ab = torch.stack([torch.rand(cin, device=dev, generator=g) + 0.5,
+                              torch.randn(cin, device=dev, generator=g) * 0.1]).contiguous()
+            kw["in_ab"] = ab
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
-            y = conv2d(conv, x)
+            y = conv2d(conv, x, **kw)
+            if mode != "plain":
+                y = torch.cat([y[0].flatten(), y[1].flatten().view(torch.bfloat16)]) \
+                    if y[1] is not None else y[0]
             torch.cuda.synchronize()
             reps = 10
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(reps):
-                conv2d(conv, x)
+                conv2d(conv, x, **kw)
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / reps
         tot += ms * count
         torch.save(y.cpu(), os.path.join(out_dir, f"y{li}.pt"))
         print(json.dumps({"lib": lib, "cin": cin, "hw": h, "cout": cout, "k": k, "stride": s,
-                          "ms": round(ms, 4), "tflops": round(flop / ms / 1e9, 1)}), flush=True)
-    print(json.dumps({"lib": lib, "layers_3_4_ms_per_image": round(tot, 4)}), flush=True)
+                          "mode": mode, "ms": round(ms, 4), "tflops": round(flop / ms / 1e9, 1)}), flush=True)
+    key = "layer2_ms_per_image" if os.environ.get("AB_SET") == "layer2" else "layers_3_4_ms_per_image"
+    print(json.dumps({"lib": lib, key: round(tot, 4)}), flush=True)
 
 
 def main():
@@ -60,18 +84,21 @@ def main():
     dirs = []
     for lib in libs:
         d = tempfile.mkdtemp(prefix="abconv_")
-        env = dict(os.environ, MCGMIL_LIB=os.path.abspath(lib), AB_CHILD=d)
+        path, *sets = lib.split("+")
+        env = dict(os.environ, MCGMIL_LIB=os.path.abspath(path), AB_CHILD=d,
+                   AB_TAG="".join("+" + kv for kv in sets))
+        env.update(kv.split("=", 1) for kv in sets)
         rc = subprocess.call([sys.executable, os.path.abspath(__file__)], env=env)
         if rc != 0:
             print(json.dumps({"lib": lib, "rc": rc}))
             return rc
         dirs.append(d)
     ok = True
-    for li in range(len(LAYERS)):
+    for li in range(len(layers())):
         ref = torch.load(os.path.join(dirs[0], f"y{li}.pt"), weights_only=True)
         for d, lib in zip(dirs[1:], libs[1:]):
             y = torch.load(os.path.join(d, f"y{li}.pt"), weights_only=True)
-            eq = bool(torch.equal(y, ref))
+            eq = bool(torch.equal(y.view(torch.int16), ref.view(torch.int16)))   # bits (NaN-safe)
             ok &= eq
             if not eq:
                 print(json.dumps({"layer": li, "lib": lib, "bitwise": False,

@@ -19,8 +19,10 @@ for s in ${STEPS:-smoke calib all bench}; do
         fused) step pytest_fused 300 python -u -m pytest tests/test_gpu_fused.py -m gpu -x -q -rf --timeout 120 --timeout-method thread ;;
         all) step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
         cfg5) step bench_cfg5 600 python bench.py --workload cfg5 --steps 5 --warmup 2 --no-cpu-baseline ;;
-        profcfg5) rm -rf "$OUT/prof_cfg5"; step rocprof_cfg5 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg5" -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 2 --warmup 1 --no-cpu-baseline
-              find "$OUT/prof_cfg5" -name "*kernel_trace.csv" -exec cp {} "$OUT/kernel_trace_cfg5.csv" \; ;;
+        profcfg5) rm -rf "$OUT/prof_cfg5"; step rocprof_cfg5 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg5" -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 2 --warmup 1 --no-cpu-baseline --no-calibration
+              find "$OUT/prof_cfg5" -name "*kernel_trace.csv" -exec cp {} "$OUT/kernel_trace_cfg5.csv" \;
+              find "$OUT/prof_cfg5" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_cfg5.csv" \;
+              python3 scripts/cfg5_phase_table.py "$OUT/kernel_trace_cfg5.csv" "$OUT/cfg5_phases.json" ;;
         pmcconv) step pmc_conv 1100 env PROBE_K=1507 PMC_CMD="python3 scripts/probe_conv.py" PASSES="sq lds coex" bash scripts/pmc_passes.sh ;;
         parity) step pytest_parity 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fused.py -m gpu -x -q -rf --timeout 300 --timeout-method thread ;;
         bench) step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;

@@ -43,7 +43,7 @@ def test_library_targets_gfx950(hip_lib):
 
 def test_args_struct_matches_binding(hip_lib):
     from mcgmil import _lib
-    assert hip_lib.mcgmil_abi_version() == 5 == _lib.ABI_VERSION
+    assert hip_lib.mcgmil_abi_version() == 6 == _lib.ABI_VERSION
     assert hip_lib.mcgmil_conv_args_size() == ctypes.sizeof(_lib.ConvArgs)
     assert hip_lib.mcgmil_stem_args_size() == ctypes.sizeof(_lib.StemArgs)
     assert hip_lib.mcgmil_args_size() == ctypes.sizeof(_lib.Args)
@@ -299,6 +299,36 @@ def test_conv_stats_parts_and_validation(hip_lib):
     assert p.value == 0
     assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 64, 3, 1, 1, flags=4)), ctypes.byref(p)) == -1
     assert hip_lib.mcgmil_conv_stats_parts(ctypes.byref(conv(64, 64, 3, 1, 1, reserved=1)), ctypes.byref(p)) == -1
+
+
+def test_conv_workspace_size(hip_lib):
+    """mcgmil_conv_workspace_size: the K split of the last 256 x 256 tiles (without a GPU the plan
+    assumes 256 CUs). Config 5's layer 4 (k = 1,507, 7 x 7 x 512: 289 pixel tiles per channel tile
+    over 128 workgroup rows) cuts its 33 left tiles into 3 K ranges: 33 x 2 channel tiles x 3
+    ranges of 256 x 256 fp32 sums; layer 3 (1,154 tiles over 256 rows: 130 left, 1 range per row)
+    and the 1x1 (4 K steps) take none, nor do kernels other than the 256 x 256 one."""
+    from mcgmil import _lib
+    n = ctypes.c_size_t()
+
+    def conv(cin, cout, k, s, pad, hw, batch=1507, **kw):
+        a = _lib.ConvArgs()
+        a.batch, a.height, a.width, a.in_channels = batch, hw, hw, cin
+        a.out_channels, a.kernel_h, a.kernel_w, a.stride, a.pad = cout, k, k, s, pad
+        for key, v in kw.items():
+            setattr(a, key, v)
+        return a
+    for args, want in ((conv(512, 512, 3, 1, 1, 7), 33 * 2 * 3 * 256 * 256 * 4),
+                       (conv(256, 512, 3, 2, 1, 14), 33 * 2 * 3 * 256 * 256 * 4),
+                       (conv(256, 512, 1, 2, 0, 14), 0), (conv(256, 256, 3, 1, 1, 14), 0),
+                       (conv(128, 128, 3, 1, 1, 28), 0), (conv(512, 512, 3, 1, 1, 7, flags=2), 0),
+                       (conv(512, 512, 3, 1, 1, 7, batch=2), 0)):
+        assert hip_lib.mcgmil_conv_workspace_size(ctypes.byref(args), ctypes.byref(n)) == 0
+        assert n.value == want, (args.in_channels, args.width, args.batch, n.value)
+    assert hip_lib.mcgmil_conv_workspace_size(ctypes.byref(conv(512, 512, 3, 1, 1, 7)), None) == -1
+    assert hip_lib.mcgmil_conv_workspace_size(ctypes.byref(conv(48, 512, 3, 1, 1, 7)), ctypes.byref(n)) == -2
+    # a misaligned workspace is refused before anything launches
+    bad = conv(512, 512, 3, 1, 1, 7, x=4096, w=4096, y=4096, workspace=4096 + 16, workspace_bytes=1 << 30)
+    assert hip_lib.mcgmil_conv2d(ctypes.byref(bad), None) == -3
 
 
 def test_batchnorm_coefficients_validation(hip_lib):

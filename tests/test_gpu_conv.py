@@ -112,6 +112,55 @@ def test_conv2d_tile_policy_flags(cuda, shape):
         assert torch.all(err <= 2.0 ** -8 * ref.abs() + 1e-5 * mag), name
 
 
+# 256 x 256 tiles with a short last round (on 256 CUs: 14 x 14 -> 256, 307 tiles over 256 rows, 51
+# left in 4 K ranges; 7 x 7 x 512 and its stride-2 producer, 134 tiles over 128 rows, 6 left in 4)
+SPLIT_SHAPES = [(400, 256, 14, 14, 256, 3, 1, 1), (700, 512, 7, 7, 512, 3, 1, 1), (700, 256, 14, 14, 512, 3, 2, 1)]
+
+
+@pytest.mark.parametrize("shape", SPLIT_SHAPES)
+def test_conv2d_k_split(cuda, shape, monkeypatch):
+    """The K split of the last round of 256 x 256 tiles (mcgmil_conv_args.workspace): within the
+    fp64 bound and repeatable; the whole tiles bitwise those of the unsplit launch
+    (MCGMIL_CONV_SPLIT=0, no workspace), the split tiles at most one bf16 rounding from them."""
+    import ctypes
+    from mcgmil import _lib
+    from mcgmil.features import _conv_args, conv2d
+    N, Cin, H, W, Cout, k, s, p = shape
+    conv = _layer(Cin, Cout, k, s, p, cuda, Cin + 3 * Cout + k)
+    g = torch.Generator(device=cuda).manual_seed(N + H)
+    x = torch.randn(N, Cin, H, W, device=cuda, generator=g).relu_().bfloat16()
+    x = x.contiguous(memory_format=torch.channels_last)
+    nb = ctypes.c_size_t()
+    assert _lib.load().mcgmil_conv_workspace_size(ctypes.byref(_conv_args(conv, x)), ctypes.byref(nb)) == 0
+    if nb.value == 0:
+        pytest.skip("no K split for this shape at this GPU's CU count")
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        monkeypatch.setenv("MCGMIL_CONV_SPLIT", "0")
+        y0 = conv2d(conv, x)
+        monkeypatch.setenv("MCGMIL_CONV_SPLIT", "1")
+        y1 = conv2d(conv, x)
+        y2 = conv2d(conv, x)
+    assert torch.equal(y1, y2)
+    wb = conv.weight.detach().bfloat16().double()
+    with torch.no_grad():
+        ref = F.conv2d(x.double(), wb, None, s, p)
+        mag = F.conv2d(x.double().abs(), wb.abs(), None, s, p)
+    err = (y1.double() - ref).abs()
+    assert torch.all(err <= 2.0 ** -8 * ref.abs() + 1e-5 * mag)
+    # rows (pixels) of the whole tiles: F tiles per workgroup row, tiles_n * rows <= CUs
+    cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+    tiles_m, tiles_n = (y0.numel() // Cout + 255) // 256, Cout // 256
+    rows = min(max(cus // tiles_n, 1), tiles_m)
+    whole = (tiles_m // rows) * rows * 256
+    r0 = y0.permute(0, 2, 3, 1).reshape(-1, Cout)
+    r1 = y1.permute(0, 2, 3, 1).reshape(-1, Cout)
+    assert whole < r0.shape[0]
+    assert torch.equal(r0[:whole], r1[:whole])
+    a, b = r0[whole:].double(), r1[whole:].double()
+    m = mag.permute(0, 2, 3, 1).reshape(-1, Cout)[whole:]
+    assert torch.all((a - b).abs() <= 2.0 ** -7 * torch.maximum(a.abs(), b.abs()) + 2e-5 * m)
+
+
 RING_SHAPES = [(3, 64, 56, 56, 64), (48, 64, 56, 56, 64), (120, 64, 20, 50, 64), (2, 64, 20, 62, 64)]
 
 
