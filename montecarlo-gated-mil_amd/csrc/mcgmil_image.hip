@@ -391,6 +391,60 @@ __global__ void __launch_bounds__(kThreads) gather_kernel(Geom g, int channels, 
     }
 }
 
+// The same copy walked in TILE order: block (tile, channel) in ascending tile index, the blocks
+// dealt to the 8 XCDs in contiguous chunks (guide T1, bijective form), each block writing its
+// tile's rows to the tile's bag position n = pos[rank] (rank when not shuffled). In the bag's own
+// (shuffled) order the overlapping tiles that share pixels are far apart, so every instance
+// re-read its pixels from HBM (stride ps / 4 at config 5: each pixel sits in up to 16 tiles);
+// in tile order neighbours run together on one XCD and share its L2. Same values, same places.
+#ifndef MCGMIL_GATHER_TILES
+#define MCGMIL_GATHER_TILES 1
+#endif
+#ifndef MCGMIL_GATHER_NT
+#define MCGMIL_GATHER_NT 1
+#endif
+template <typename In, typename Out, int VEC>
+__global__ void __launch_bounds__(kThreads) gather_tiles_kernel(Geom g, int channels, const In* __restrict__ img,
+                                                                long long ld_row, long long ld_ch, Ws w,
+                                                                int shuffle, long long capacity,
+                                                                const int32_t* num_selected, Norm nm,
+                                                                Out* __restrict__ out) {
+    const unsigned b = blockIdx.x, nb = gridDim.x, x8 = b & 7u, q = nb >> 3, r8 = nb & 7u;
+    const long long L = (long long)(x8 < r8 ? x8 * (q + 1) : r8 * (q + 1) + (x8 - r8) * q) + (b >> 3);
+    const long long i = L / channels;
+    const int ch = (int)(L - i * channels);
+    const int rk = w.rank[i];
+    if (rk >= *num_selected) return;
+    const long long n = shuffle ? w.pos[rk] : rk;
+    if (n >= capacity) return;
+    const int ps = g.ps;
+    const int ty = w.ys[i / g.nx], tx = w.xs[i % g.nx];
+    const In* src = img + ch * ld_ch + (long long)ty * ld_row + tx;
+    Out* dst = out + (n * channels + ch) * ps * ps;
+    const float m = nm.on ? nm.mean[ch] : 0.f, sd = nm.on ? nm.std[ch] : 1.f;
+    const int x0 = (threadIdx.x & 31) * VEC;
+#pragma unroll 4
+    for (int r = threadIdx.x >> 5; r < ps; r += kThreads / 32) {
+        for (int x = x0; x < ps; x += 32 * VEC) {
+            const vec_t<In, VEC> v = *reinterpret_cast<const vec_t<In, VEC>*>(src + (long long)r * ld_row + x);
+            vec_t<Out, VEC> o;
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                float f = (float)v[e];
+                if (nm.on) f = (f - m) / sd;
+                o[e] = to_out<Out>(f);
+            }
+#if MCGMIL_GATHER_NT
+            if constexpr (sizeof(vec_t<Out, VEC>) == 16)
+                __builtin_nontemporal_store(__builtin_bit_cast(vec_t<uint32_t, 4>, o),
+                                            reinterpret_cast<vec_t<uint32_t, 4>*>(dst + (long long)r * ps + x));
+            else
+#endif
+                *reinterpret_cast<vec_t<Out, VEC>*>(dst + (long long)r * ps + x) = o;
+        }
+    }
+}
+
 // Ordered list (instance order) of the instances whose tile covers the cell with top-left
 // (y0, x0), built in LDS chunk by chunk with ballot compaction. Returns the count.
 __device__ int collect_cover(const Geom& g, const Ws& w, const int32_t* ids, int k, int y0, int x0,
@@ -584,6 +638,19 @@ int launch_gather(const Geom& g, const mcgmil_image_args* a, const Ws& w, hipStr
                       (a->channels == 1 || a->ld_channel % 8 == 0) && g.ps % 8 == 0 && g.stride % 8 == 0 &&
                       (g.W - g.ps) % 8 == 0 && ((uintptr_t)a->instances % (8 * sizeof(Out))) == 0;
     const dim3 grid((unsigned)blocks), block(kThreads);
+    if (MCGMIL_GATHER_TILES && g.tiles() * a->channels < (1ll << 31)) {
+        const dim3 tgrid((unsigned)(g.tiles() * a->channels));
+        const int sh = a->shuffle ? 1 : 0;
+        if (vec8)
+            hipLaunchKernelGGL((gather_tiles_kernel<In, Out, 8>), tgrid, block, 0, s, g, a->channels,
+                               (const In*)a->image, (long long)a->ld_row, (long long)a->ld_channel, w, sh,
+                               (long long)a->instance_capacity, a->num_selected, nm, (Out*)a->instances);
+        else
+            hipLaunchKernelGGL((gather_tiles_kernel<In, Out, 1>), tgrid, block, 0, s, g, a->channels,
+                               (const In*)a->image, (long long)a->ld_row, (long long)a->ld_channel, w, sh,
+                               (long long)a->instance_capacity, a->num_selected, nm, (Out*)a->instances);
+        return check_launch("gather_tiles_kernel");
+    }
     if (vec8)
         hipLaunchKernelGGL((gather_kernel<In, Out, 8>), grid, block, 0, s, g, a->channels, (const In*)a->image,
                            (long long)a->ld_row, (long long)a->ld_channel, w, a->tile_ids, a->num_selected, nm,
