@@ -4,6 +4,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <set>
 #include <string>
@@ -174,6 +175,39 @@ int launch_gate_generic(const mcgmil::GateParams& gp, hipStream_t s) {
     return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_scores_kernel launch");
 }
 
+int device_cus() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+    if (dev < 64) {
+        const int c = cache[dev].load(std::memory_order_relaxed);
+        if (c > 0) return c;
+    }
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    if (dev < 64) cache[dev].store(cus, std::memory_order_relaxed);
+    return cus;
+}
+
+// Short tiles for a sparse last round (bf16, two gate pairs per wave: the reference's separate
+// heads). gate_pipe_kernel holds one workgroup per CU, so `tiles` 128-row tiles run in
+// ceil(tiles / CUs) rounds; when the last round would fill at most half the CUs (one bag per call:
+// N = 2,048, T = 100 is 1,600 tiles = 6.25 rounds; T = 50 3.125) its rows go to a second launch of
+// 32- or 64-row tiles (rows' scores bitwise the same), at most one round of them.
+// MCGMIL_SHORT_TILES=0 in the environment: whole tiles only (A/B timing; read once per process).
+int short_tile_rows(long long tiles) {
+    static const bool off = [] {
+        const char* e = getenv("MCGMIL_SHORT_TILES");
+        return e && strcmp(e, "0") == 0;
+    }();
+    if (off) return 0;
+    const long long cus = device_cus(), full = tiles / cus * cus, rem = tiles - full;
+    if (full == 0 || rem == 0) return 0;
+    if (4 * rem <= cus) return 32;
+    if (2 * rem <= cus) return 64;
+    return 0;
+}
+
 template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE>
 int launch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
     auto* k = &mcgmil::gate_pipe_kernel<E, PPW, MAXC, REPLAY, ONE>;
@@ -186,9 +220,28 @@ int launch_gate_pipe(const mcgmil::GateParams& gp, hipStream_t s) {
     if (gp.uniform_rows <= 0)
         if (int rc = launch_plan(gp, mcgmil::kPipeBM, s)) return rc;
     const size_t lds = mcgmil::pipe_lds_bytes<E, MAXC>();
-    hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(mcgmil::kGateThreads), lds, s, gp);
+    int srows = 0;
+    if constexpr (sizeof(E) == 2 && PPW == 2)
+        if (!gp.clock) srows = short_tile_rows(tiles);
+    const long long main_tiles = srows ? tiles / device_cus() * device_cus() : tiles;
+    hipLaunchKernelGGL(k, dim3((unsigned)main_tiles), dim3(mcgmil::kGateThreads), lds, s, gp);
     hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MCGMIL_OK : hip_fail(e, "gate_pipe_kernel launch");
+    if (e != hipSuccess) return hip_fail(e, "gate_pipe_kernel launch");
+    if constexpr (sizeof(E) == 2 && PPW == 2) {
+        if (srows) {
+            mcgmil::GateParams gt = gp;
+            gt.tile_row0 = main_tiles * mcgmil::kPipeBM;
+            const long long n = (gp.total_samples - gt.tile_row0 + srows - 1) / srows;
+            auto* ks = srows == 32 ? &mcgmil::gate_pipe_kernel<E, PPW, MAXC, REPLAY, ONE, false, 2>
+                                   : &mcgmil::gate_pipe_kernel<E, PPW, MAXC, REPLAY, ONE, false, 4>;
+            if (int rc = mcgmil_detail::raise_lds_limit(reinterpret_cast<const void*>(ks), "gate_pipe_kernel LDS limit"))
+                return rc;
+            hipLaunchKernelGGL(ks, dim3((unsigned)n), dim3(mcgmil::kGateThreads), lds, s, gt);
+            e = hipGetLastError();
+            if (e != hipSuccess) return hip_fail(e, "gate_pipe_kernel (short tiles) launch");
+        }
+    }
+    return MCGMIL_OK;
 }
 
 template <typename E, int RT, int PPW, int MAXC, bool REPLAY, bool ONE>
@@ -451,6 +504,7 @@ int gate_params(const mcgmil_args* a, mcgmil::GateParams& gp) {
     gp.clock = (a->flags & MCGMIL_CLOCK_PROBE) ? static_cast<unsigned long long*>(a->debug) : nullptr;
 #endif
     gp.tile_bag = reinterpret_cast<const int32_t*>(static_cast<char*>(a->workspace) + l.plan_off);
+    gp.tile_row0 = 0;
     gp.uniform_rows = a->uniform_bag_rows;
     gp.Y = a->Y;
     gp.A = a->A;

@@ -50,6 +50,7 @@ struct GateParams {
     int region_t;                  // t-groups per region when every bag has uniform_rows rows
     unsigned long long* stamps;    // diagnostic build only: [tiles][8] s_memtime stamps
     unsigned long long* clock;     // MCGMIL_CLOCK_PROBE: [kClockSlots][4] clock record, or nullptr
+    long long tile_row0;           // short-tile launches (gate_pipe_kernel RTV < 8): first row
 };
 
 // The clock probe (MCGMIL_CLOCK_PROBE): thread 0 of workgroups 0..kClockSlots-1 writes
@@ -92,12 +93,13 @@ constexpr int kRowInfo = 6;        // ints per row: hrow, t, n, bag, Nb, bag cou
 
 // Row table of one BM-row tile of the flattened (bag, t, n) space (threads < BM). With a tile
 // plan (bag of the tile's first row) a row walks forward over at most the few bags that start
-// inside the tile instead of binary-searching the CSR offsets (dependent L2 loads).
-template <int BM>
+// inside the tile instead of binary-searching the CSR offsets (dependent L2 loads). Rows from RV
+// on are padding (a short tile: its first RV rows only).
+template <int BM, int RV = BM>
 __device__ __forceinline__ void fill_row_table(const GateParams& p, long long R0, int* rinfo) {
     const int tid = threadIdx.x;
     if (tid >= BM) return;
-    const long long R = R0 + tid;
+    const long long R = tid < RV ? R0 + tid : p.total_samples;
     int hrow = -1, t = 0, n = 0, bag = 0, Nb = 0;
     // 32-bit unsigned division when the launch's sample rows fit (wave-uniform branch); the
     // 64-bit one is a ~50-instruction software routine
@@ -199,7 +201,7 @@ __device__ __forceinline__ void load_head_vectors(const GateParams& p, int q0, i
 // rt*16 + (lane & 15) and d = 16*db + 4*(lane >> 4) + v (16x16 C layout, weights as A).
 // ONE_CLASS: every pair of this wave belongs to gate g and feeds class g only (separate
 // heads): one accumulator, part[0]. Otherwise part[c] for every class (shared gate).
-template <int RT, int PPW, int MAXC, bool ONE_CLASS>
+template <int RT, int PPW, int MAXC, bool ONE_CLASS, int RTV = RT>
 __device__ __forceinline__ void fold_pairs(const GateParams& p, const f32x4 (&acc)[RT][2 * PPW],
                                            int q0, int lane, float (&part)[MAXC][RT],
                                            const HeadVec* pre = nullptr) {
@@ -234,7 +236,7 @@ __device__ __forceinline__ void fold_pairs(const GateParams& p, const f32x4 (&ac
             }
         }
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
+        for (int rt = 0; rt < RTV; ++rt) {           // row tiles past RTV: a short tile's padding
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
                 const float ax = fmaf(acc[rt][2 * jp][v], av_s, bvv[v]);
@@ -631,8 +633,11 @@ __device__ __forceinline__ void load_classifier_lds(__amdgpu_buffer_rsrc_t wrs, 
 // One 128-row tile of the flattened (bag, t, n) space, rows R0 .. R0+127, whose row table is
 // already in `rinfo` (and visible: the caller's barrier). Scores go to lg_out / z_out at row
 // R0 + r - obase. LDS: Xs [2][SLOT] staging slots, red / zred the cross-wave reductions.
+// RTV < 8 (a short tile, gate_pipe_kernel's tail launch): row tiles RTV.. are padding -- no
+// MFMAs, no staging, no H loads and no epilogue for them; every row computes exactly as in a full
+// tile (same K order, same cross-wave sum), so the scores are bitwise the same.
 template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS, bool EARLY_HV = true,
-          bool ZL = false, bool ZLOAD = true>
+          bool ZL = false, bool ZLOAD = true, int RTV = kPipeBM / 16>
 __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* Xs, float* red,
                                           float* zred, const int* rinfo, float* lg_out,
                                           float* z_out, long long obase, E* zw = nullptr) {
@@ -720,10 +725,10 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
 #if MCGMIL_DIAG & 1   // ablation (timing only, wrong results): no H prefetch
         hn = h;
 #else
-        hn = load_raw(hsrc + (size_t)sh * 32);
+        if (RTV == RT || wave < RTV) hn = load_raw(hsrc + (size_t)sh * 32);
 #endif
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
+        for (int rt = 0; rt < RTV; ++rt) {
             const Frag<E> x = load_frag(cur + (size_t)(rt * 64 + lane) * 8);
 #pragma unroll
             for (int j = 0; j < NJ; ++j) acc[rt][j] = mma(w[j], x, acc[rt][j]);
@@ -731,7 +736,7 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
         const Frag<E> xz = load_frag(cur + (size_t)tid * 8);  // row tile `wave`
         if constexpr (ZL) zacc = mma(load_frag(zw + (size_t)(s * 64 + lane) * 8), xz, zacc);
         else zacc = mma(z, xz, zacc);
-        stage(s + 1, h, nxt);           // step KS is staged into the idle slot and never read
+        if (RTV == RT || wave < RTV) stage(s + 1, h, nxt);   // step KS: the idle slot, never read
         if constexpr (sizeof(E) == 2 && PPW == 2) {
             // Spread the Philox/staging VALU over the MFMA stream (1 MFMA : VPM VALU) instead
             // of one block after it: the two waves of a SIMD run the step in lockstep, so a
@@ -753,7 +758,7 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
             __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
 #else
 #pragma unroll
-            for (int i = 0; i < RT * NJ + 1; ++i) {
+            for (int i = 0; i < RTV * NJ + 1; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
                 __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0); // VALU
             }
@@ -774,9 +779,11 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
     {
         // prologue: stage step 0, load the weights of step 0 and H of step 1
         Frag<E> wA[NJ], wB[NJ], zA, zB;
-        Raw<E> hA, hB;
-        hA = load_raw(hsrc);
-        hB = load_raw(hsrc + 32);
+        Raw<E> hA{}, hB{};
+        if (RTV == RT || wave < RTV) {
+            hA = load_raw(hsrc);
+            hB = load_raw(hsrc + 32);
+        }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) wA[j] = wfrag(wsoff[j]);
         if constexpr (ZL) {
@@ -787,7 +794,7 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
         } else {
             zA = wfrag(zsoff);
         }
-        stage(0, hA, Xs);
+        if (RTV == RT || wave < RTV) stage(0, hA, Xs);
         __syncthreads();
         MCGMIL_STAMP(p, 2);
 
@@ -812,7 +819,7 @@ __device__ __forceinline__ void pipe_tile(const GateParams& p, long long R0, E* 
     for (int c = 0; c < MAXC; ++c)
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) part[c][rt] = 0.f;
-    fold_pairs<RT, PPW, MAXC, ONE_CLASS>(p, acc, q0, lane, part, kEarlyHV ? hvec : nullptr);
+    fold_pairs<RT, PPW, MAXC, ONE_CLASS, RTV>(p, acc, q0, lane, part, kEarlyHV ? hvec : nullptr);
     MCGMIL_STAMP(p, 4);
     // ONE_CLASS: the wave's pairs all belong to gate q0 / (D/16) (idle waves: class >= C)
     const int one_class = ONE_CLASS ? (q0 < p.P ? q0 / (p.D >> 4) : MAXC) : -1;
@@ -846,7 +853,9 @@ __device__ __forceinline__ long long xcd_tile(unsigned b, unsigned n, int bags) 
 #endif
 }
 
-template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS, bool PROBE = false>
+// RTV < 8: the tail launch of short tiles (16 RTV rows each from p.tile_row0), so that a last
+// round of tiles that would leave most CUs idle is spread over them (launch_gate_pipe)
+template <typename E, int PPW, int MAXC, bool REPLAY, bool ONE_CLASS, bool PROBE = false, int RTV = kPipeBM / 16>
 __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int BM = kPipeBM;
@@ -854,14 +863,16 @@ __global__ __launch_bounds__(kGateThreads) void gate_pipe_kernel(const GateParam
     float* red = reinterpret_cast<float*>(smem + (size_t)pipe_slots<E>() * BM * 32 * sizeof(E));
     float* zred = red + red_floats<BM, MAXC>();
     int* rinfo = reinterpret_cast<int*>(zred + MAXC * BM);
-    const long long R0 = xcd_tile(blockIdx.x, gridDim.x, p.B) * BM;
+    const long long R0 = RTV == BM / 16 ? xcd_tile(blockIdx.x, gridDim.x, p.B) * BM
+                                        : p.tile_row0 + (long long)blockIdx.x * (16 * RTV);
 
     if constexpr (PROBE) clock_probe(p, 0);
     MCGMIL_STAMP(p, 0);
-    fill_row_table<BM>(p, R0, rinfo);
+    fill_row_table<BM, 16 * RTV>(p, R0, rinfo);
     __syncthreads();
     MCGMIL_STAMP(p, 1);
-    pipe_tile<E, PPW, MAXC, REPLAY, ONE_CLASS>(p, R0, Xs, red, zred, rinfo, p.logits, p.zz, 0);
+    pipe_tile<E, PPW, MAXC, REPLAY, ONE_CLASS, true, false, true, RTV>(p, R0, Xs, red, zred, rinfo, p.logits,
+                                                                       p.zz, 0);
     if constexpr (PROBE) clock_probe(p, 1);
 }
 
