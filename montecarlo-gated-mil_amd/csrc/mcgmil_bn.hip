@@ -60,6 +60,13 @@ __device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
 #ifndef MCGMIL_BN_MAXBLOCKS
 #define MCGMIL_BN_MAXBLOCKS 4096
 #endif
+// bn_vpool_col_kernel walks its columns LAST image first: the stem wrote the activation in image
+// order, so its most recent part still sits in the 256 MB Infinity Cache when the pass starts
+// (same values, same places): 360-364 -> 352-353 us at config 5 (profiles/r06/bnrev/kernel_stats_*.csv). The same
+// reversal of bn_apply_kernel's walk measured no change (201-202 us). 0: first image first.
+#ifndef MCGMIL_BN_REVERSE
+#define MCGMIL_BN_REVERSE 1
+#endif
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void load8s(const __bf16* p, float (&v)[8]) {
 #if MCGMIL_BN_NT
@@ -430,8 +437,9 @@ __global__ __launch_bounds__(kThreads) void bn_vpool_col_kernel(const __bf16* __
                                                                 const float* __restrict__ ab) {
     const int CG = C >> 3;
     const long long rs = (long long)Wp * C;          // elements per (pooled-width) row
-    for (long long col = (long long)blockIdx.x * kThreads + threadIdx.x; col < ncol;
-         col += (long long)gridDim.x * kThreads) {
+    for (long long walk = (long long)blockIdx.x * kThreads + threadIdx.x; walk < ncol;
+         walk += (long long)gridDim.x * kThreads) {
+        const long long col = MCGMIL_BN_REVERSE ? ncol - 1 - walk : walk;   // last image first
         const int cg = (int)(col % CG);
         const long long t = col / CG;
         const int pw = (int)(t % Wp);
