@@ -154,6 +154,22 @@ def test_empty_and_capped_bags(cuda):
     assert inst.shape[0] == 7 and idx.tolist() == list(range(7))   # all 100%: index order
 
 
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_capped_bag_instances_in_bag_order(cuda, shuffle):
+    """A capped bag (bag_size < the tiles above the threshold), shuffled or not, at the 8-wide and
+    scalar gathers: instance n holds the crop of tile idx[n]. The gather walks the tiles in tile
+    order and writes each selected tile to its bag position (gather_tiles_kernel)."""
+    from mcgmil.patcher import ImagePatcher
+    for h, w, ps, ov in ((300, 248, 32, 0.75), (150, 137, 20, 0.5)):
+        img = synthetic_image(21, h, w, 3)
+        p = ImagePatcher(patch_size=ps, overlap=ov, bag_size=9, empty_thresh=0.2)
+        tiles = p.get_tiles(h, w)
+        inst, idx, _ = p.convert_img_to_bag(torch.from_numpy(img).to(cuda), shuffle=shuffle, seed=3)
+        px = P.nonzero_percent(img, tiles)
+        assert len(idx) == 9 and sorted(idx.tolist()) == sorted(P.select(px, 0.2, 9).tolist())
+        assert torch.equal(inst.cpu(), P.crops(img, tiles, idx))
+
+
 def test_patch_size_equal_to_image(cuda):
     """ps == H == W gives the reference's duplicated tile (start points [0, 0])."""
     from mcgmil.patcher import ImagePatcher
