@@ -125,16 +125,18 @@ class ImagePatcher:
             for i in range(c):
                 a.norm_mean[i], a.norm_std[i] = float(mean[i]), float(std[i])
         px = torch.empty(nt, dtype=torch.float32, device=dev)
-        ids = torch.empty(nt, dtype=torch.int32, device=dev)
-        count = torch.empty(1, dtype=torch.int32, device=dev)
+        # k and the bag's tile ids in one buffer, so one copy (one host sync) brings both back
+        sel = torch.empty(nt + 1, dtype=torch.int32, device=dev)
+        count, ids = sel[:1], sel[1:]
         inst = torch.empty(cap, c, self.patch_size, self.patch_size, dtype=out_dtype, device=dev)
         a.px, a.tile_ids, a.num_selected = _p(px), _p(ids), _p(count)
         a.instances, a.instance_capacity = _p(inst), cap
         ws = _workspace(L, a, dev)  # noqa: F841  (kept alive until the launch is queued)
         _lib.check(L.mcgmil_image_to_bag(ctypes.byref(a), _stream(dev)), "mcgmil_image_to_bag")
-        k = int(count.item())
+        host = sel.cpu().numpy()
+        k = int(host[0])
         self.last_px, self.last_tile_ids = px, ids[:k]
-        idx = ids[:k].cpu().numpy().astype(np.int64)
+        idx = host[1:1 + k].astype(np.int64)
         return inst[:k], idx, self.tiles[idx, 4:6]
 
     # -- reconstruction ------------------------------------------------------------------
