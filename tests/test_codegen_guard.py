@@ -27,7 +27,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "montecarlo-gated-mil_amd"))
 
 HIPCC = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
-HEADLINE = "_ZN6mcgmil16gate_pipe_kernelIDF16bLi2ELi2ELb0ELb1ELb0EEEvNS_10GateParamsE"
+HEADLINE = "_ZN6mcgmil16gate_pipe_kernelIDF16bLi2ELi2ELb0ELb1ELb0ELi8EEEvNS_10GateParamsE"   # RTV = 8: whole tiles
 FUSED = "_ZN6mcgmil17gate_fused_kernelIDF16bLi2ELi2ELb1ELb0EEEvNS_10GateParamsE"
 # the MCGMIL_CLOCK_PROBE instantiations (same loop code + two stamps) fit as well
 HEADLINE_PROBE = HEADLINE.replace("Lb1ELb0EEEv", "Lb1ELb1EEEv")
