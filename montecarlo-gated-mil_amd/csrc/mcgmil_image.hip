@@ -317,20 +317,24 @@ __global__ void __launch_bounds__(kThreads) scatter_kernel(Geom g, int cap, Ws w
 
 // The bag order. shuffle: position of rank r = #{r' < k : key_r' < key_r or (== and r' < r)},
 // key_r = Philox4x32-10(counter {r, 0, 0, "SHFL"}, key = seed) word 0 -- a seeded permutation
-// standing in for sklearn.utils.shuffle (image_patcher.py:131). Same 2-D split as rank_kernel.
+// standing in for sklearn.utils.shuffle (image_patcher.py:131). A 2-D split like rank_kernel's,
+// with kShuffleChunk-key chunks: k is only known on the device (k <= tiles), so most blocks of
+// the (tiles/256) x (tiles/kShuffleChunk) grid exit at once and the rest each compare 64 keys
+// (integer atomics: order-free).
+constexpr int kShuffleChunk = 64;
 __global__ void __launch_bounds__(kThreads) shuffle_rank_kernel(uint32_t k0, uint32_t k1,
                                                                 const int32_t* num_selected, Ws w) {
-    __shared__ uint32_t s_key[kThreads];
+    __shared__ uint32_t s_key[kShuffleChunk];
     const int k = *num_selected;
-    const int base = blockIdx.y * kThreads;
+    const int base = blockIdx.y * kShuffleChunk;
     if (base >= k) return;                       // uniform per block
-    const int j = base + threadIdx.x;
-    s_key[threadIdx.x] = philox4x32_10((uint32_t)j, 0u, 0u, kShuffleTag, k0, k1).x;
+    if (threadIdx.x < kShuffleChunk)
+        s_key[threadIdx.x] = philox4x32_10((uint32_t)(base + threadIdx.x), 0u, 0u, kShuffleTag, k0, k1).x;
     __syncthreads();
     const int r = blockIdx.x * kThreads + threadIdx.x;
     if (r >= k) return;
     const uint32_t kr = philox4x32_10((uint32_t)r, 0u, 0u, kShuffleTag, k0, k1).x;
-    const int m = min(kThreads, k - base);
+    const int m = min(kShuffleChunk, k - base);
     int pos = 0;
     for (int jj = 0; jj < m; ++jj) {
         const uint32_t q = s_key[jj];
@@ -748,7 +752,8 @@ int mcgmil_image_to_bag(const mcgmil_image_args* a, void* stream) {
     hipLaunchKernelGGL(scatter_kernel, dim3(tb), dim3(kThreads), 0, s, g, cap, w, a->px, a->num_selected);
     if ((rc = check_launch("scatter_kernel"))) return rc;
     if (a->shuffle) {
-        hipLaunchKernelGGL(shuffle_rank_kernel, dim3(tb, tb), dim3(kThreads), 0, s, (uint32_t)a->shuffle_seed,
+        const unsigned tc = (unsigned)((nt + kShuffleChunk - 1) / kShuffleChunk);
+        hipLaunchKernelGGL(shuffle_rank_kernel, dim3(tb, tc), dim3(kThreads), 0, s, (uint32_t)a->shuffle_seed,
                            (uint32_t)(a->shuffle_seed >> 32), a->num_selected, w);
         if ((rc = check_launch("shuffle_rank_kernel"))) return rc;
     }
