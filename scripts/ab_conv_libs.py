@@ -22,9 +22,16 @@ LAYERS2 = [(128, 28, 128, 3, 1, 1, 0, "plain"), (128, 28, 128, 3, 1, 1, 1, "stat
            (128, 28, 128, 3, 1, 1, 2, "xf")]
 
 
+# layer 2's 1x1 / stride-2 downsample from 64 channels (conv1x1_kernel), with statistics as config 5
+# runs it
+LAYERS_DOWN = [(64, 56, 128, 1, 2, 0, 1, "stats"), (64, 56, 128, 1, 2, 0, 0, "plain")]
+
+
 def layers():
     if os.environ.get("AB_SET") == "layer2":
         return LAYERS2
+    if os.environ.get("AB_SET") == "down":
+        return LAYERS_DOWN
     return [t + ("plain",) for t in LAYERS]
 
 
@@ -72,7 +79,8 @@ def child(out_dir):
         torch.save(y.cpu(), os.path.join(out_dir, f"y{li}.pt"))
         print(json.dumps({"lib": lib, "cin": cin, "hw": h, "cout": cout, "k": k, "stride": s,
                           "mode": mode, "ms": round(ms, 4), "tflops": round(flop / ms / 1e9, 1)}), flush=True)
-    key = "layer2_ms_per_image" if os.environ.get("AB_SET") == "layer2" else "layers_3_4_ms_per_image"
+    key = {"layer2": "layer2_ms_per_image", "down": "downsample_ms_per_image"}.get(
+        os.environ.get("AB_SET"), "layers_3_4_ms_per_image")
     print(json.dumps({"lib": lib, key: round(tot, 4)}), flush=True)
 
 
