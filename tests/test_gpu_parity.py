@@ -129,6 +129,29 @@ def test_bf16_drift_vs_fp32_reference(cuda):
     compare(case, run(case, cuda, torch.bfloat16), TOL_BF16_VS_FP32)
 
 
+@pytest.mark.parametrize("T", [17, 21])
+def test_replay_equals_philox_with_short_tiles(cuda, T):
+    """One bag of N = 2,048 at T = 17 / 21: 272 / 336 128-row tiles, so on 256 CUs the last round
+    runs as 32- / 64-row short tiles (gate_pipe_kernel<..., RTV>). Replaying the kernel's own
+    Philox masks (keep_feat / keep_att from feature_keep / attention_keep) gives bitwise the
+    outputs of the in-kernel draws, through both the REPLAY and the Philox short-tile
+    instantiations."""
+    from mcgmil import ops
+    N, L, C, seed, base = 2048, 512, 2, 0x5EED, 11
+    sd = synthetic.head_state_dict(3, L=L, D=128, C=C, shared=False)
+    head = head_on(synthetic.head_arrays(sd, C, False), cuda)
+    H = torch.from_numpy(synthetic.bag_features(8, N, L)).to(cuda).bfloat16().contiguous()
+    offs = ops.bag_offsets_tensor([N], cuda)
+    kw = dict(p_feat=0.25, p_att=0.1, seed=seed, bag_id_base=base, return_stats=True)
+    a = ops.mcdo_forward(H, offs, head, T, **kw)
+    kf = ops.feature_keep(offs, N, T, L, 0.25, seed, bag_id_base=base)
+    ka = ops.attention_keep(offs, N, T, C, 0.1, seed, bag_id_base=base)
+    b = ops.mcdo_forward(H, offs, head, T, keep_feat=kf, keep_att=ka, **kw)
+    torch.cuda.synchronize()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
 @pytest.mark.parametrize("name", ["small_N64_T4_sep", "edge_N37_T5_shared", "cfg2_N512_T30_sep"])
 def test_bf16_replay_matches_oracle(cuda, name):
     case = Case(name)
