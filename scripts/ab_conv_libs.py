@@ -22,9 +22,10 @@ LAYERS2 = [(128, 28, 128, 3, 1, 1, 0, "plain"), (128, 28, 128, 3, 1, 1, 1, "stat
            (128, 28, 128, 3, 1, 1, 2, "xf")]
 
 
-# layer 2's 1x1 / stride-2 downsample from 64 channels (conv1x1_kernel), with statistics as config 5
-# runs it
-LAYERS_DOWN = [(64, 56, 128, 1, 2, 0, 1, "stats"), (64, 56, 128, 1, 2, 0, 0, "plain")]
+# layer 2's stride-2 convolutions from 64 channels: the 1x1 downsample (conv1x1_kernel) and the 3x3
+# (conv_dma_kernel<256, 128>), with statistics as config 5 runs them, and plain
+LAYERS_DOWN = [(64, 56, 128, 1, 2, 0, 1, "stats"), (64, 56, 128, 1, 2, 0, 0, "plain"),
+               (64, 56, 128, 3, 2, 1, 1, "stats"), (64, 56, 128, 3, 2, 1, 0, "plain")]
 
 
 def layers():
